@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""bench.py -- MRays/s of the hot path (Trace -> Scatter -> Scene::HitScene) on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched by torch.distributed.run, one rank per GPU.  One *step* = one full
+frame of BASELINE.json configs[3]: sponza.obj 1920x1080, 64 spp (the
+deterministic stand-in scene, data/gen_standin_sponza.py; the real sponza.obj
+is absent from the reference), pixel-mode seeding, wavefront engine.  The frame
+is sharded over the N GPUs in 16-row bands dealt round-robin (total work fixed:
+strong scaling); each rank renders its bands straight into a device tensor and
+one RCCL gather over xGMI assembles the image on rank 0 -- inside the timed
+region.  value = all rays of all ranks / max-over-ranks wall time.
+
+Rank 0 prints ONE JSON line.  Besides the contract keys it carries
+  roofline      dominant kernel (extend = closest-hit traversal): algorithmic
+                bytes per launch (B_ray = 32 + 16 + 64*N_node +
+                36*N_tri, N_node/N_tri measured by an instrumented run of the same
+                kernel on the same frame at reduced spp) / its mean launch time,
+                HIP-event timed on the stream the kernel runs on; peak 8 TB/s
+  cpu_baseline  the CPU restatement of the reference algorithm (octree +
+                Moller-Trumbore, oracle/, bit-exact to the reference binary on the
+                pinned cases) timed on this host on a bounded row sample of the same
+                frame, N=1 only
+Everything else goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "data"))
+
+import numpy as np  # noqa: E402
+
+import toymeshpathtracer_amd as tm  # noqa: E402  (imports torch first: one HIP runtime)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "MRays/s on sponza.obj 1920x1080 64spp at 1/2/4/8 GPUs; %HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+BAND_ROWS = 16
+S_NODE = 64            # bytes per visited BVH2 node in our layout (both child boxes + links)
+S_TRI = 36             # bytes per triangle test (3 x vec3), SURVEY.md §8d
+S_RAY = 32 + 16        # ray read + hit write, SURVEY.md §8d
+
+CONFIGS = {
+    # name: (obj, width, height, spp, is_sponza)
+    "sponza1080": ("sponza", 1920, 1080, 64, True),    # BASELINE configs[3]: the metric's config
+    "teapot720": ("teapot.obj", 1280, 720, 16, False),  # configs[2]
+    "suzanne360": ("suzanne.obj", 640, 360, 4, False),  # configs[1]
+    "sponza4k": ("sponza", 3840, 2160, 256, True),      # configs[4] (8-GPU config)
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def scene_path(obj: str) -> str:
+    if obj == "sponza":
+        import gen_standin_sponza
+        return gen_standin_sponza.ensure()
+    return os.path.join(ROOT, "data", obj)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
+    ap.add_argument("--engine", default="wavefront", choices=["wavefront", "mega"])
+    ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
+    ap.add_argument("--cpu-row-step", type=int, default=64, help="CPU baseline: every k-th row")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--save", default="", help="rank 0 writes the frame as PNG here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+
+    obj, W, H, SPP, sponza = CONFIGS[args.config]
+    path = scene_path(obj)
+    engine = tm.ENGINE_WAVEFRONT if args.engine == "wavefront" else tm.ENGINE_MEGAKERNEL
+    tris, bmin, bmax = tm.load_scene(path)
+    cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
+    t0 = time.perf_counter()
+    scene = tm.Scene(tris, device=local)
+    init_s = time.perf_counter() - t0
+    st0 = scene.stats()
+
+    rows_of = [tm.tile_row_to_y(W, H, BAND_ROWS, s, world) for s in range(world)]
+    max_rows = max(len(r) for r in rows_of)
+    my_rows = len(rows_of[rank])
+    tile = torch.zeros((max_rows, W, 4), dtype=torch.uint8, device=dev)
+    gathered = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
+    image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    row_index = [torch.as_tensor(r, device=dev) for r in rows_of] if rank == 0 else None
+
+    def step():
+        _, rays = scene.trace_image(cam, W, H, SPP, seed_mode=tm.SEED_PIXEL, engine=engine,
+                                    band_rows=BAND_ROWS, shard=rank, num_shards=world,
+                                    out=tile.data_ptr())
+        st = scene.stats()
+        if world > 1:
+            dist.gather(tile, gathered, dst=0)
+        if rank == 0:  # de-interleave the bands into the frame, on the device
+            parts = gathered if world > 1 else [tile]
+            for s in range(world):
+                image.index_copy_(0, row_index[s], parts[s][: len(rows_of[s])])
+        return rays, st
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    ext_ms = sh_ms = 0.0
+    ext_rays = sh_rays = 0
+    ext_launches = 0
+    for _ in range(args.steps):
+        r, st = step()
+        rays += r
+        ext_ms += st.extend_ms
+        sh_ms += st.shadow_ms
+        ext_rays += st.extend_rays
+        sh_rays += st.shadow_rays
+        ext_launches += st.extend_launches
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays], dtype=torch.int64, device=dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays = int(r.item())
+
+    value = rays / elapsed / 1e6
+    if rank != 0:
+        scene.close()
+        dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (extend), from an instrumented run
+    frame = image.cpu().numpy()
+    _, _ = scene.trace_image(cam, W, H, args.count_spp, seed_mode=tm.SEED_PIXEL, engine=engine,
+                             band_rows=BAND_ROWS, shard=rank, num_shards=world,
+                             count_visits=True, out=tile.data_ptr())
+    cs = scene.stats()
+    roof = None
+    if engine == tm.ENGINE_WAVEFRONT and cs.extend_rays and ext_launches:
+        n_node = cs.node_visits / cs.extend_rays
+        n_tri = cs.tri_tests / cs.extend_rays
+        n_node_s = cs.shadow_node_visits / max(cs.shadow_rays, 1)
+        n_tri_s = cs.shadow_tri_tests / max(cs.shadow_rays, 1)
+        b_ray = S_RAY + S_NODE * n_node + S_TRI * n_tri
+        per_launch_rays = ext_rays / ext_launches
+        avg_launch_ms = ext_ms / ext_launches
+        achieved = b_ray * per_launch_rays / (avg_launch_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_wf_trace<closest-hit> (extend)",
+                "bytes_per_ray": round(b_ray, 1), "n_node_per_ray": round(n_node, 2),
+                "n_tri_per_ray": round(n_tri, 2), "avg_launch_ms": round(avg_launch_ms, 4),
+                "rays_per_launch": round(per_launch_rays, 1),
+                "shadow_bytes_per_ray": round(S_RAY + S_NODE * n_node_s + S_TRI * n_tri_s, 1),
+                "extend_ms_per_step": round(ext_ms / args.steps, 2),
+                "shadow_ms_per_step": round(sh_ms / args.steps, 2)}
+
+    # ---- CPU baseline: the reference algorithm on this host, bounded row sample
+    cpu = None
+    parity = None
+    if world == 1 and not args.no_cpu:
+        import oracle
+        threads = min(16, os.cpu_count() or 1)
+        osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
+        t1 = time.perf_counter()
+        ref, crays = osc.render(cam.as_array(), W, H, SPP, seed_mode=oracle.SEED_PIXEL,
+                                row_step=args.cpu_row_step, threads=threads)
+        cdt = time.perf_counter() - t1
+        rows = np.arange(0, H, args.cpu_row_step)
+        cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads,
+               "kind": "port",
+               "sample": f"rows y%{args.cpu_row_step}==0 ({len(rows)} x {W} px x {SPP} spp, "
+                         f"{crays} rays, {cdt:.1f} s), octree restatement of scene.cpp, pixel seeding"}
+        diff = int((frame[rows] != ref[rows]).any(-1).sum())
+        parity = {"rows_checked": int(len(rows)), "pixels_differ": diff,
+                  "oracle": "octree (reference tie order)"}
+
+    if args.save:
+        tm.write_png(args.save, frame)
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "MRays/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: deterministic stand-in for the absent sponza.obj (66,452 tris incl. "
+                "floor, data/gen_standin_sponza.py)" if sponza else "data/*.obj from the reference",
+        "config": {"workload": f"{args.config}: {os.path.basename(path)} {W}x{H} {SPP}spp",
+                   "global_batch": W * H, "spp": SPP, "tris": int(tris.shape[0]),
+                   "seed_mode": "pixel", "engine": args.engine,
+                   "parallelism": f"row-bands{BAND_ROWS}x{world}",
+                   "rays_per_step": rays // args.steps},
+        "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity,
+        "scene_init_s": round(init_s, 3), "bvh_build_ms": round(st0.build_ms, 2),
+        "bvh_depth": st0.bvh_depth,
+    }
+    print(json.dumps(out), flush=True)
+    scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,137 @@
+/*
+ * tmpt.h -- C ABI of libtmpt.so, the MI355X-native (gfx950) hot path of
+ * pr0g/ToyMeshPathTracer: Trace() -> Scatter() -> Scene::HitScene().
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes
+ * (0 = ok, < 0 = error; message in tmpt_last_error()), no C++ exceptions and no
+ * torch types cross this boundary.  Every entry point names the reference
+ * interface it replaces (/root/reference/source/<file>:<line>); INTEGRATION.md
+ * shows the reference-side binding.
+ *
+ * Threading: one scene per device.  Calls on different scenes may run from
+ * different host threads at once; one scene handle is not re-entrant for
+ * concurrent render calls.  Host buffers are caller-owned; device memory is
+ * library-owned unless a flag says the caller passes a device pointer.
+ */
+#ifndef TMPT_H
+#define TMPT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMPT_ABI_VERSION 1
+
+typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
+
+/* Camera, field for field maths.h:106-111 */
+typedef struct {
+    float origin[3], lower_left[3], horizontal[3], vertical[3], u[3], v[3], w[3];
+    float lens_radius;
+} tmpt_camera;
+
+enum { TMPT_SEED_ROW = 0, TMPT_SEED_PIXEL = 1 };
+
+/* render engines */
+enum {
+    TMPT_ENGINE_WAVEFRONT = 0,  /* generate/extend/shade/shadow kernels over compacted queues */
+    TMPT_ENGINE_MEGAKERNEL = 1  /* one lane per pixel (pixel mode) or per row (row mode) */
+};
+
+/* render flags */
+enum {
+    TMPT_FLAG_OUT_DEVICE = 1,    /* rgba_out is a device pointer on the scene's device */
+    TMPT_FLAG_COUNT_VISITS = 2   /* instrumented traversal: node visits / triangle tests */
+};
+
+/* One render call = one shard of one frame (TraceImageBody over its rows,
+ * main.cpp:180-246).  Rows are grouped in bands of band_rows rows; this call
+ * renders the bands b with b % num_shards == shard, in increasing b, into a
+ * compact tile of full-width rows (RGBA8, row 0 = the lowest rendered row,
+ * as in the reference's in-memory image, main.cpp:229).  band_rows = 0 means
+ * one band of the whole height. */
+typedef struct {
+    int32_t width, height, spp;
+    int32_t seed_mode;  /* TMPT_SEED_ROW (main.cpp:204) or TMPT_SEED_PIXEL */
+    int32_t band_rows;
+    int32_t shard, num_shards;
+    int32_t engine;
+    int32_t flags;
+    int32_t reserved[7];
+} tmpt_render_desc;
+
+/* Statistics of the last render on a scene (HIP-event timed on the scene's
+ * stream, i.e. the stream the kernels are launched on). */
+typedef struct {
+    double render_ms;             /* first kernel to last kernel of the call */
+    double extend_ms, shadow_ms;  /* summed closest-hit / any-hit kernel time */
+    uint64_t extend_rays, shadow_rays;
+    int64_t extend_launches, shadow_launches, iterations;
+    uint64_t node_visits, tri_tests; /* extend (closest-hit) kernel, with TMPT_FLAG_COUNT_VISITS */
+    uint64_t shadow_node_visits, shadow_tri_tests; /* shadow (any-hit) kernel, same flag */
+    double build_ms;                 /* LBVH build of the scene */
+    int32_t bvh_nodes, bvh_depth, n_tris, device;
+} tmpt_stats;
+
+/* ---- host side: scene ingest and camera (not kernels) ------------------- */
+
+/* LoadScene (main.cpp:122-170) over objParseFile (objparser.cpp:304-355):
+ * positions of every face, fan-triangulated, plus the 2 floor triangles.
+ * *out_tris = n*9 floats (caller frees with tmpt_free); bounds are of the OBJ
+ * triangles only (main.cpp:132-151).  Returns 0, or <0 if the file can't be read. */
+int tmpt_load_obj(const char* path, float** out_tris, int32_t* out_n, float out_bmin[3],
+                  float out_bmax[3]);
+void tmpt_free(void* p);
+
+/* Camera::Camera (maths.cpp:40-59) */
+int tmpt_camera_init(tmpt_camera* cam, const float look_from[3], const float look_at[3],
+                     const float vup[3], float vfov, float aspect, float aperture,
+                     float focus_dist);
+/* camera placement of main.cpp:295-307 (is_sponza: strstr(path,"sponza.obj")) */
+int tmpt_camera_for_scene(tmpt_camera* cam, const float bmin[3], const float bmax[3],
+                          int32_t width, int32_t height, int32_t is_sponza);
+
+/* ---- device side --------------------------------------------------------- */
+
+int tmpt_device_count(void);
+
+/* Scene::Scene (scene.h:19, scene.cpp:97-100) + Scene::BuildOctree
+ * (scene.h:26, scene.cpp:118-126): copies n triangles (n*9 floats, v0 v1 v2)
+ * to `device` and builds the LBVH there.  The caller keeps ownership of tris. */
+int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene** out);
+/* Scene::~Scene (scene.h:20) */
+int tmpt_scene_destroy(tmpt_scene* scene);
+
+/* Scene::HitScene (scene.h:36-37, scene.cpp:129-140), batched:
+ * rays = n x {orig.xyz, dir.xyz} (dir normalised), hits = n x {pos.xyz,
+ * normal.xyz, t} written where ids[i] >= 0; ids[i] = index of the closest
+ * triangle or -1 (the reference returns 1 instead of the index).  any_hit != 0
+ * stops at the first accepted triangle (the shadow query's semantics: only
+ * ids[i] >= 0 is meaningful).  Host pointers. */
+int tmpt_scene_hit(const tmpt_scene* scene, const float* rays, int64_t n, float tmin, float tmax,
+                   int32_t any_hit, float* hits, int32_t* ids);
+
+/* tbb::parallel_for(rows, TraceImageBody) (main.cpp:329-331, 180-246):
+ * renders desc's shard into rgba_out (tmpt_tile_rows(desc) * width * 4 bytes).
+ * *ray_count = every HitScene call (main.cpp:57,91), counted in uint64. */
+int tmpt_render(tmpt_scene* scene, const tmpt_camera* cam, const tmpt_render_desc* desc,
+                uint8_t* rgba_out, uint64_t* ray_count);
+/* rows in the tile of desc's shard; global row of tile row r */
+int32_t tmpt_tile_rows(const tmpt_render_desc* desc);
+int32_t tmpt_tile_row_to_y(const tmpt_render_desc* desc, int32_t r);
+
+int tmpt_get_stats(const tmpt_scene* scene, tmpt_stats* out);
+
+/* PNG writer (stbi_write_png with flip-on-write, main.cpp:341-342):
+ * rgba rows bottom-up as rendered. */
+int tmpt_write_png(const char* path, const uint8_t* rgba, int32_t width, int32_t height);
+
+const char* tmpt_last_error(void);
+int tmpt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMPT_H */

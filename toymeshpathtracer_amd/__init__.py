@@ -1,0 +1,348 @@
+"""toymeshpathtracer_amd -- MI355X-native (gfx950) hot path of pr0g/ToyMeshPathTracer.
+
+Python face of ``libtmpt.so`` (C ABI: ``include/tmpt.h``), mirroring the
+reference's host interface for the path (``/root/reference/source``):
+
+==========================  ==============================================
+reference                   here
+==========================  ==============================================
+``LoadScene`` main.cpp:122  :func:`load_scene`
+``Camera`` maths.cpp:40     :class:`Camera` (+ :meth:`Camera.for_scene`, main.cpp:295-307)
+``Scene`` scene.h:17        :class:`Scene` (LBVH on the GPU)
+``Scene::HitScene`` :36     :meth:`Scene.hit_scene` / :meth:`Scene.hit_scene_batch`
+``TraceImageBody`` :180     :meth:`Scene.trace_image` (parallel_for, main.cpp:329)
+``stbi_write_png`` :342     :func:`write_png`
+==========================  ==============================================
+
+The compute path is the HIP library only: if ``libtmpt.so`` is missing this
+module raises on import -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+__all__ = [
+    "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
+    "SEED_ROW", "SEED_PIXEL", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "lib_path", "TmptError",
+    "tile_rows", "tile_row_to_y",
+]
+
+SEED_ROW, SEED_PIXEL = 0, 1
+ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL = 0, 1
+FLAG_OUT_DEVICE, FLAG_COUNT_VISITS = 1, 2
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(_HERE, "_lib", "libtmpt.so")
+
+
+class TmptError(RuntimeError):
+    pass
+
+
+if not os.path.exists(lib_path):
+    raise ImportError(
+        f"libtmpt.so not built ({lib_path}); run `python -c 'import __graft_entry__ as g; g.build()'` "
+        "or `make -C toymeshpathtracer_amd/csrc`. There is no CPU fallback.")
+
+# One HIP runtime per process: torch wheels bundle their own libamdhip64 /
+# libhsa-runtime64 (same sonames as /opt/rocm's).  Importing torch first makes
+# libtmpt bind to the runtime torch already loaded, so torch CUDA tensors,
+# torch.distributed (RCCL) and our kernels share one device context.  Without
+# torch, the system ROCm runtime is used.
+try:  # pragma: no cover - depends on the environment
+    import torch  # noqa: F401
+except Exception:  # torch is optional for the C ABI itself
+    torch = None
+
+_lib = ctypes.CDLL(lib_path)
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class _Camera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("lower_left", ctypes.c_float * 3),
+                ("horizontal", ctypes.c_float * 3), ("vertical", ctypes.c_float * 3),
+                ("u", ctypes.c_float * 3), ("v", ctypes.c_float * 3), ("w", ctypes.c_float * 3),
+                ("lens_radius", ctypes.c_float)]
+
+
+class _Desc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("seed_mode", ctypes.c_int32), ("band_rows", ctypes.c_int32),
+                ("shard", ctypes.c_int32), ("num_shards", ctypes.c_int32),
+                ("engine", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 7)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("render_ms", ctypes.c_double), ("extend_ms", ctypes.c_double),
+                ("shadow_ms", ctypes.c_double), ("extend_rays", ctypes.c_uint64),
+                ("shadow_rays", ctypes.c_uint64), ("extend_launches", ctypes.c_int64),
+                ("shadow_launches", ctypes.c_int64), ("iterations", ctypes.c_int64),
+                ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64),
+                ("shadow_node_visits", ctypes.c_uint64), ("shadow_tri_tests", ctypes.c_uint64),
+                ("build_ms", ctypes.c_double), ("bvh_nodes", ctypes.c_int32),
+                ("bvh_depth", ctypes.c_int32), ("n_tris", ctypes.c_int32),
+                ("device", ctypes.c_int32)]
+
+
+def _sig(name, res, args):
+    fn = getattr(_lib, name)
+    fn.restype = res
+    fn.argtypes = args
+    return fn
+
+
+_load_obj = _sig("tmpt_load_obj", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_f32p), _i32p, _f32p, _f32p])
+_free = _sig("tmpt_free", None, [ctypes.c_void_p])
+_cam_init = _sig("tmpt_camera_init", ctypes.c_int, [ctypes.POINTER(_Camera), _f32p, _f32p, _f32p,
+                                                     ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                     ctypes.c_float])
+_cam_scene = _sig("tmpt_camera_for_scene", ctypes.c_int, [ctypes.POINTER(_Camera), _f32p, _f32p,
+                                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32])
+_dev_count = _sig("tmpt_device_count", ctypes.c_int, [])
+_scene_create = _sig("tmpt_scene_create", ctypes.c_int, [_f32p, ctypes.c_int32, ctypes.c_int32,
+                                                         ctypes.POINTER(ctypes.c_void_p)])
+_scene_destroy = _sig("tmpt_scene_destroy", ctypes.c_int, [ctypes.c_void_p])
+_scene_hit = _sig("tmpt_scene_hit", ctypes.c_int, [ctypes.c_void_p, _f32p, ctypes.c_int64,
+                                                   ctypes.c_float, ctypes.c_float, ctypes.c_int32,
+                                                   _f32p, _i32p])
+_render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Camera),
+                                             ctypes.POINTER(_Desc), ctypes.c_void_p, _u64p])
+_tile_rows = _sig("tmpt_tile_rows", ctypes.c_int32, [ctypes.POINTER(_Desc)])
+_tile_row_to_y = _sig("tmpt_tile_row_to_y", ctypes.c_int32, [ctypes.POINTER(_Desc), ctypes.c_int32])
+_stats = _sig("tmpt_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Stats)])
+_write_png = _sig("tmpt_write_png", ctypes.c_int, [ctypes.c_char_p, _u8p, ctypes.c_int32, ctypes.c_int32])
+_last_error = _sig("tmpt_last_error", ctypes.c_char_p, [])
+_abi = _sig("tmpt_abi_version", ctypes.c_int, [])
+
+#: every symbol include/tmpt.h declares (checked by tests/test_abi.py)
+EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_scene",
+           "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_destroy", "tmpt_scene_hit",
+           "tmpt_render", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
+           "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise TmptError(f"{what} failed ({rc}): {_last_error().decode(errors='replace')}")
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_f32p)
+
+
+def device_count() -> int:
+    return int(_dev_count())
+
+
+def abi_version() -> int:
+    return int(_abi())
+
+
+# ----------------------------------------------------------------------------- scene ingest
+def load_scene(path: str) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """LoadScene (main.cpp:122-170): returns (tris[n,3,3] float32 incl. the 2
+    floor triangles, bounds_min[3], bounds_max[3]) -- bounds of the OBJ only."""
+    p = _f32p()
+    n = ctypes.c_int32()
+    bmin = np.zeros(3, np.float32)
+    bmax = np.zeros(3, np.float32)
+    _check(_load_obj(path.encode(), ctypes.byref(p), ctypes.byref(n), _fp(bmin), _fp(bmax)),
+           f"load_scene({path!r})")
+    try:
+        tris = np.ctypeslib.as_array(p, shape=(n.value * 9,)).copy().reshape(n.value, 3, 3)
+    finally:
+        _free(p)
+    return tris, bmin, bmax
+
+
+# ----------------------------------------------------------------------------- camera
+@dataclass
+class Camera:
+    """Camera of maths.h:83-112 (fields as computed by Camera::Camera)."""
+    origin: np.ndarray
+    lower_left: np.ndarray
+    horizontal: np.ndarray
+    vertical: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    w: np.ndarray
+    lens_radius: float
+
+    @staticmethod
+    def _from_c(c: _Camera) -> "Camera":
+        a = lambda f: np.array(list(f), np.float32)
+        return Camera(a(c.origin), a(c.lower_left), a(c.horizontal), a(c.vertical), a(c.u),
+                      a(c.v), a(c.w), float(c.lens_radius))
+
+    def _to_c(self) -> _Camera:
+        c = _Camera()
+        for name in ("origin", "lower_left", "horizontal", "vertical", "u", "v", "w"):
+            getattr(c, name)[:] = [float(x) for x in np.asarray(getattr(self, name), np.float32)]
+        c.lens_radius = self.lens_radius
+        return c
+
+    @staticmethod
+    def create(look_from, look_at, vup, vfov: float, aspect: float, aperture: float,
+               focus_dist: float) -> "Camera":
+        """Camera::Camera (maths.cpp:40-59)."""
+        c = _Camera()
+        lf, la, up = (np.asarray(x, np.float32) for x in (look_from, look_at, vup))
+        _check(_cam_init(ctypes.byref(c), _fp(lf), _fp(la), _fp(up), vfov, aspect, aperture,
+                         focus_dist), "Camera")
+        return Camera._from_c(c)
+
+    @staticmethod
+    def for_scene(bmin, bmax, width: int, height: int, is_sponza: bool = False) -> "Camera":
+        """Camera placement of main.cpp:295-307."""
+        c = _Camera()
+        lo, hi = np.asarray(bmin, np.float32), np.asarray(bmax, np.float32)
+        _check(_cam_scene(ctypes.byref(c), _fp(lo), _fp(hi), width, height, int(is_sponza)),
+               "Camera.for_scene")
+        return Camera._from_c(c)
+
+    def as_array(self) -> np.ndarray:
+        return np.concatenate([self.origin, self.lower_left, self.horizontal, self.vertical,
+                               self.u, self.v, self.w, [self.lens_radius]]).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- scene
+@dataclass
+class Hit:
+    """Hit of maths.h:46-51."""
+    pos: np.ndarray
+    normal: np.ndarray
+    t: float
+
+
+@dataclass
+class RenderStats:
+    render_ms: float
+    extend_ms: float
+    shadow_ms: float
+    extend_rays: int
+    shadow_rays: int
+    extend_launches: int
+    shadow_launches: int
+    iterations: int
+    node_visits: int
+    tri_tests: int
+    shadow_node_visits: int
+    shadow_tri_tests: int
+    build_ms: float
+    bvh_nodes: int
+    bvh_depth: int
+    n_tris: int
+    device: int
+
+
+def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
+          engine=ENGINE_WAVEFRONT, flags=0) -> _Desc:
+    d = _Desc()
+    d.width, d.height, d.spp, d.seed_mode = width, height, spp, seed_mode
+    d.band_rows, d.shard, d.num_shards = band_rows, shard, num_shards
+    d.engine, d.flags = engine, flags
+    return d
+
+
+def tile_rows(width, height, band_rows=0, shard=0, num_shards=1) -> int:
+    return int(_tile_rows(ctypes.byref(_desc(width, height, 1, 0, band_rows, shard, num_shards))))
+
+
+def tile_row_to_y(width, height, band_rows, shard, num_shards) -> np.ndarray:
+    d = _desc(width, height, 1, 0, band_rows, shard, num_shards)
+    n = int(_tile_rows(ctypes.byref(d)))
+    return np.array([_tile_row_to_y(ctypes.byref(d), r) for r in range(n)], np.int64)
+
+
+class Scene:
+    """Scene (scene.h:17-43): triangles copied to the GPU, LBVH built there
+    (replaces Scene::BuildOctree, scene.cpp:118-126)."""
+
+    def __init__(self, triangles: np.ndarray, device: int = 0):
+        tris = np.ascontiguousarray(np.asarray(triangles, np.float32).reshape(-1, 9))
+        self._h = ctypes.c_void_p()
+        self.n = tris.shape[0]
+        self.device = device
+        _check(_scene_create(_fp(tris), self.n, device, ctypes.byref(self._h)), "Scene")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _scene_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- Scene::HitScene (scene.cpp:129-140)
+    def hit_scene_batch(self, rays: np.ndarray, t_min: float, t_max: float,
+                        any_hit: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+        """rays [n,6] (orig, dir) -> (ids[n] triangle index or -1, hits[n,7] pos/normal/t)."""
+        rays = np.ascontiguousarray(np.asarray(rays, np.float32).reshape(-1, 6))
+        n = rays.shape[0]
+        hits = np.zeros((n, 7), np.float32)
+        ids = np.full(n, -1, np.int32)
+        _check(_scene_hit(self._h, _fp(rays), n, t_min, t_max, int(any_hit), _fp(hits),
+                          ids.ctypes.data_as(_i32p)), "hit_scene")
+        return ids, hits
+
+    def hit_scene(self, orig, direction, t_min: float, t_max: float) -> Tuple[int, Optional[Hit]]:
+        """Same contract as the reference: returns (-1, None) on a miss and
+        (1, Hit) on a hit (scene.cpp:81 returns 1, not the index)."""
+        ids, hits = self.hit_scene_batch(np.concatenate([orig, direction])[None], t_min, t_max)
+        if ids[0] < 0:
+            return -1, None
+        h = hits[0]
+        return 1, Hit(h[0:3].copy(), h[3:6].copy(), float(h[6]))
+
+    # -- TraceImageBody over parallel_for (main.cpp:180-246, 329-331)
+    def trace_image(self, camera: Camera, width: int, height: int, spp: int,
+                    seed_mode: int = SEED_ROW, engine: int = ENGINE_WAVEFRONT, band_rows: int = 0,
+                    shard: int = 0, num_shards: int = 1, count_visits: bool = False,
+                    out=None) -> Tuple[np.ndarray, int]:
+        """Render one shard.  Returns (rgba[tile_rows, width, 4] uint8, rays).
+        Row 0 is the lowest rendered row (main.cpp:229; flipped on PNG write).
+        ``out`` may be a device pointer (int) with tile_rows*width*4 bytes."""
+        d = _desc(width, height, spp, seed_mode, band_rows, shard, num_shards, engine,
+                  (FLAG_COUNT_VISITS if count_visits else 0) | (FLAG_OUT_DEVICE if out is not None else 0))
+        rows = int(_tile_rows(ctypes.byref(d)))
+        rays = ctypes.c_uint64()
+        cam = camera._to_c()
+        if out is not None:
+            _check(_render(self._h, ctypes.byref(cam), ctypes.byref(d), ctypes.c_void_p(int(out)),
+                           ctypes.byref(rays)), "trace_image")
+            return None, int(rays.value)
+        img = np.zeros((rows, width, 4), np.uint8)
+        _check(_render(self._h, ctypes.byref(cam), ctypes.byref(d), img.ctypes.data_as(ctypes.c_void_p),
+                       ctypes.byref(rays)), "trace_image")
+        return img, int(rays.value)
+
+    def stats(self) -> RenderStats:
+        s = _Stats()
+        _check(_stats(self._h, ctypes.byref(s)), "stats")
+        return RenderStats(*[getattr(s, f) for f, _ in _Stats._fields_])
+
+
+def write_png(path: str, rgba: np.ndarray) -> None:
+    """stbi_write_png with flip-on-write (main.cpp:341-342): rgba rows bottom-up."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    h, w = rgba.shape[:2]
+    _check(_write_png(path.encode(), rgba.ctypes.data_as(_u8p), w, h), "write_png")

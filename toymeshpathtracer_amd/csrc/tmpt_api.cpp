@@ -1,0 +1,284 @@
+// tmpt_api.cpp -- the C ABI of include/tmpt.h.  Status ints cross the
+// boundary; no exception escapes (every entry point catches).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "tmpt.h"
+#include "tmpt_internal.h"
+
+namespace tmpt {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+const char* last_error() { return g_last_error.c_str(); }
+
+int load_obj(const char* path, std::vector<float>& tris, f3& bmin, f3& bmax);
+void camera_init(tmpt_camera* cam, f3 lookFrom, f3 lookAt, f3 vup, float vfov, float aspect,
+                 float aperture, float focusDist);
+void camera_for_scene(tmpt_camera* cam, f3 sceneMin, f3 sceneMax, int w, int h, bool sponza);
+int write_png(const char* path, const uint8_t* rgba, int w, int h);
+int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t* d_out,
+           uint64_t* ray_count);
+int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
+                    float* d_hits, int32_t* d_ids);
+
+}  // namespace tmpt
+
+struct tmpt_scene {
+    tmpt::Scene s;
+};
+
+using namespace tmpt;
+
+#define TMPT_GUARD_BEGIN try {
+#define TMPT_GUARD_END                                  \
+    }                                                   \
+    catch (const std::bad_alloc&) {                     \
+        set_error("out of host memory");                \
+        return -1;                                      \
+    }                                                   \
+    catch (...) {                                       \
+        set_error("unexpected C++ exception");          \
+        return -1;                                      \
+    }
+
+namespace {
+int bad(const char* msg)
+{
+    set_error(msg);
+    return -22;
+}
+}  // namespace
+
+extern "C" {
+
+int tmpt_abi_version(void) { return TMPT_ABI_VERSION; }
+const char* tmpt_last_error(void) { return last_error(); }
+void tmpt_free(void* p) { free(p); }
+
+int tmpt_load_obj(const char* path, float** out_tris, int32_t* out_n, float out_bmin[3],
+                  float out_bmax[3])
+{
+    TMPT_GUARD_BEGIN
+    if (!path || !out_tris || !out_n) return bad("tmpt_load_obj: null argument");
+    std::vector<float> tris;
+    f3 bmin, bmax;
+    int rc = load_obj(path, tris, bmin, bmax);
+    if (rc) return rc;
+    float* p = (float*)malloc(tris.size() * sizeof(float));
+    if (!p) return bad("tmpt_load_obj: out of memory");
+    memcpy(p, tris.data(), tris.size() * sizeof(float));
+    *out_tris = p;
+    *out_n = (int32_t)(tris.size() / 9);
+    if (out_bmin) { out_bmin[0] = bmin.x; out_bmin[1] = bmin.y; out_bmin[2] = bmin.z; }
+    if (out_bmax) { out_bmax[0] = bmax.x; out_bmax[1] = bmax.y; out_bmax[2] = bmax.z; }
+    return 0;
+    TMPT_GUARD_END
+}
+
+int tmpt_camera_init(tmpt_camera* cam, const float lf[3], const float la[3], const float up[3],
+                     float vfov, float aspect, float aperture, float focus_dist)
+{
+    if (!cam || !lf || !la || !up) return bad("tmpt_camera_init: null argument");
+    camera_init(cam, mk(lf[0], lf[1], lf[2]), mk(la[0], la[1], la[2]), mk(up[0], up[1], up[2]),
+                vfov, aspect, aperture, focus_dist);
+    return 0;
+}
+
+int tmpt_camera_for_scene(tmpt_camera* cam, const float bmin[3], const float bmax[3],
+                          int32_t width, int32_t height, int32_t is_sponza)
+{
+    if (!cam || !bmin || !bmax) return bad("tmpt_camera_for_scene: null argument");
+    if (width < 1 || height < 1) return bad("tmpt_camera_for_scene: bad size");
+    camera_for_scene(cam, mk(bmin[0], bmin[1], bmin[2]), mk(bmax[0], bmax[1], bmax[2]), width,
+                     height, is_sponza != 0);
+    return 0;
+}
+
+int tmpt_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene** out)
+{
+    TMPT_GUARD_BEGIN
+    if (!out || n < 0 || (n > 0 && !tris)) return bad("tmpt_scene_create: bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    TMPT_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return bad("tmpt_scene_create: no such device");
+    TMPT_HIP(hipSetDevice(device));
+    tmpt_scene* h = new tmpt_scene();
+    Scene& s = h->s;
+    s.device = device;
+    s.n = n;
+    auto fail = [&](int rc) {
+        tmpt_scene_destroy(h);
+        return rc;
+    };
+    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess)
+        return fail((set_error("hipStreamCreate failed"), -1));
+    s.sincos = device_sincos_table(device);
+    if (!s.sincos) return fail(-1);
+    float* d_tris = nullptr;
+    if (n > 0) {
+        if (hipMalloc(&d_tris, sizeof(float) * 9 * (size_t)n) != hipSuccess)
+            return fail((set_error("tmpt_scene_create: out of device memory"), -1));
+        if (hipMemcpy(d_tris, tris, sizeof(float) * 9 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d_tris);
+            return fail((set_error("tmpt_scene_create: upload failed"), -1));
+        }
+    }
+    int rc = build_lbvh(s, d_tris);
+    if (d_tris) (void)hipFree(d_tris);
+    if (rc) return fail(rc);
+    *out = h;
+    return 0;
+    TMPT_GUARD_END
+}
+
+int tmpt_scene_destroy(tmpt_scene* h)
+{
+    if (!h) return 0;
+    Scene& s = h->s;
+    (void)hipSetDevice(s.device);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.nodes) (void)hipFree(s.nodes);
+    if (s.tri_pre) (void)hipFree(s.tri_pre);
+    if (s.tri_orig) (void)hipFree(s.tri_orig);
+    if (s.ws) (void)hipFree(s.ws);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    delete h;
+    return 0;
+}
+
+int tmpt_scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, float tmax,
+                   int32_t any_hit, float* hits, int32_t* ids)
+{
+    TMPT_GUARD_BEGIN
+    if (!hc || n < 0 || (n > 0 && (!rays || !hits || !ids))) return bad("tmpt_scene_hit: bad arguments");
+    if (n == 0) return 0;
+    Scene& s = const_cast<tmpt_scene*>(hc)->s;
+    TMPT_HIP(hipSetDevice(s.device));
+    float *d_rays = nullptr, *d_hits = nullptr;
+    int32_t* d_ids = nullptr;
+    auto cleanup = [&]() {
+        if (d_rays) (void)hipFree(d_rays);
+        if (d_hits) (void)hipFree(d_hits);
+        if (d_ids) (void)hipFree(d_ids);
+    };
+    if (hipMalloc(&d_rays, 24 * (size_t)n) != hipSuccess || hipMalloc(&d_hits, 28 * (size_t)n) != hipSuccess ||
+        hipMalloc(&d_ids, 4 * (size_t)n) != hipSuccess) {
+        cleanup();
+        return bad("tmpt_scene_hit: out of device memory");
+    }
+    int rc = 0;
+    if (hipMemcpy(d_rays, rays, 24 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_hits, hits, 28 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
+        rc = (set_error("tmpt_scene_hit: upload failed"), -1);
+    if (!rc) rc = intersect_batch(s, d_rays, n, tmin, tmax, any_hit != 0, d_hits, d_ids);
+    if (!rc && (hipStreamSynchronize(s.stream) != hipSuccess ||
+                hipMemcpy(hits, d_hits, 28 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(ids, d_ids, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = (set_error("tmpt_scene_hit: kernel or readback failed"), -1);
+    cleanup();
+    return rc;
+    TMPT_GUARD_END
+}
+
+int32_t tmpt_tile_rows(const tmpt_render_desc* d)
+{
+    if (!d || d->height < 1) return 0;
+    int band = d->band_rows > 0 ? d->band_rows : d->height;
+    int ns = d->num_shards > 1 ? d->num_shards : 1;
+    int sh = ns > 1 ? d->shard : 0;
+    int nbands = (d->height + band - 1) / band;
+    int rows = 0;
+    for (int b = sh; b < nbands; b += ns) rows += std::min(band, d->height - b * band);
+    return rows;
+}
+
+int32_t tmpt_tile_row_to_y(const tmpt_render_desc* d, int32_t r)
+{
+    int band = d->band_rows > 0 ? d->band_rows : d->height;
+    int ns = d->num_shards > 1 ? d->num_shards : 1;
+    int sh = ns > 1 ? d->shard : 0;
+    int lb = r / band;
+    return (lb * ns + sh) * band + (r - lb * band);
+}
+
+int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d,
+                uint8_t* rgba_out, uint64_t* ray_count)
+{
+    TMPT_GUARD_BEGIN
+    if (!h || !cam || !d || !rgba_out) return bad("tmpt_render: null argument");
+    // main.cpp:258-280 argument ranges
+    if (d->width < 1 || d->width > 10000) return bad("tmpt_render: invalid width");
+    if (d->height < 1 || d->height > 10000) return bad("tmpt_render: invalid height");
+    if (d->spp < 1 || d->spp > 1024) return bad("tmpt_render: invalid samplesPerPixel");
+    if (d->seed_mode != TMPT_SEED_ROW && d->seed_mode != TMPT_SEED_PIXEL)
+        return bad("tmpt_render: invalid seed_mode");
+    if (d->engine != TMPT_ENGINE_WAVEFRONT && d->engine != TMPT_ENGINE_MEGAKERNEL)
+        return bad("tmpt_render: invalid engine");
+    if (d->num_shards > 1 && (d->shard < 0 || d->shard >= d->num_shards))
+        return bad("tmpt_render: invalid shard");
+    Scene& s = h->s;
+    TMPT_HIP(hipSetDevice(s.device));
+    const int32_t rows = tmpt_tile_rows(d);
+    const size_t bytes = (size_t)rows * (size_t)d->width * 4;
+    const bool dev_out = (d->flags & TMPT_FLAG_OUT_DEVICE) != 0;
+    uint32_t* d_out = nullptr;
+    if (dev_out) d_out = (uint32_t*)rgba_out;
+    else if (bytes && hipMalloc(&d_out, bytes) != hipSuccess) return bad("tmpt_render: out of device memory");
+    int rc = render(s, cam, d, d_out, ray_count);
+    if (!rc && !dev_out && bytes) {
+        if (hipMemcpy(rgba_out, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = (set_error("tmpt_render: readback failed"), -1);
+    }
+    if (!dev_out && d_out) (void)hipFree(d_out);
+    return rc;
+    TMPT_GUARD_END
+}
+
+int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
+{
+    if (!h || !o) return bad("tmpt_get_stats: null argument");
+    const Scene& s = h->s;
+    memset(o, 0, sizeof(*o));
+    o->render_ms = s.render_ms;
+    o->extend_ms = s.extend_ms;
+    o->shadow_ms = s.shadow_ms;
+    o->extend_rays = s.extend_rays;
+    o->shadow_rays = s.shadow_rays;
+    o->extend_launches = s.extend_launches;
+    o->shadow_launches = s.shadow_launches;
+    o->iterations = s.iterations;
+    o->node_visits = s.node_visits;
+    o->tri_tests = s.tri_tests;
+    o->shadow_node_visits = s.shadow_node_visits;
+    o->shadow_tri_tests = s.shadow_tri_tests;
+    o->build_ms = s.build_ms;
+    o->bvh_nodes = s.n_nodes;
+    o->bvh_depth = s.max_depth;
+    o->n_tris = s.n;
+    o->device = s.device;
+    return 0;
+}
+
+int tmpt_write_png(const char* path, const uint8_t* rgba, int32_t w, int32_t h)
+{
+    TMPT_GUARD_BEGIN
+    if (!path || !rgba || w < 1 || h < 1) return bad("tmpt_write_png: bad arguments");
+    return write_png(path, rgba, w, h);
+    TMPT_GUARD_END
+}
+
+}  // extern "C"

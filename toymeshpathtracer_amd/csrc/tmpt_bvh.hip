@@ -1,0 +1,482 @@
+// tmpt_bvh.hip -- on-device LBVH build for gfx950, replacing the reference's
+// octree build (Scene::BuildOctree / OctreeNode::Subdivide, scene.cpp:118-203).
+//
+// Pipeline (all on the scene's stream; DESIGN.md "LBVH build"):
+//   1. k_tri_prep     per triangle: TriOrig record (v0,v1,v2,normal), padded leaf
+//                     box, centroid; centroid bounds by block reduction + one
+//                     ordered-int atomic per block and axis
+//   2. k_morton       30-bit Morton code of the normalised centroid
+//   3. radix sort     4 x 8-bit LSD passes; per pass: tile histograms, one scan,
+//                     stable scatter ranked with wave64 ballots (no LDS atomics)
+//   4. k_karras       Karras 2012 hierarchy over (code, index) keys
+//   5. k_depth        node depth by walking parent links (<= 62 steps)
+//   6. k_refit_level  boxes bottom-up, one launch per level: the kernel boundary
+//                     is the only inter-workgroup synchronisation, so no
+//                     cross-XCD release/acquire is needed
+//   7. k_assemble     64-B nodes (both child boxes + child links) and the
+//                     leaf-ordered TriPre records
+// The build is outside the timed region of the reference (main.cpp:312 vs
+// :319) and of bench.py; it is timed separately (Scene::build_ms).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "tmpt_internal.h"
+
+namespace tmpt {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t f2ord(float f)
+{
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u)
+{
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+struct Soa6 {  // leaf or node boxes, structure of arrays for coalesced sweeps
+    float *lx, *ly, *lz, *hx, *hy, *hz;
+};
+
+__global__ void __launch_bounds__(kBlock) k_tri_prep(const float* __restrict__ tris9, int32_t n,
+                                                     TriOrig* __restrict__ orig, Soa6 box,
+                                                     float* __restrict__ cent,
+                                                     uint32_t* __restrict__ cbounds /*6*/)
+{
+    __shared__ uint32_t red[6][kBlock / 64];
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    float c[3] = {INFINITY, INFINITY, INFINITY};
+    float cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (i < n) {
+        const float* t = tris9 + 9 * (int64_t)i;
+        f3 v0 = mk(t[0], t[1], t[2]), v1 = mk(t[3], t[4], t[5]), v2 = mk(t[6], t[7], t[8]);
+        f3 nrm = tri_normal(v0, v1, v2);
+        orig[i].a = f4(v0.x, v0.y, v0.z, v1.x);
+        orig[i].b = f4(v1.y, v1.z, v2.x, v2.y);
+        orig[i].c = f4(v2.z, nrm.x, nrm.y, nrm.z);
+        f3 lo = vmin(vmin(v0, v1), v2), hi = vmax(vmax(v0, v1), v2);
+        float px = kBoxPadRel * (fmaxf(fabsf(lo.x), fabsf(hi.x)) + (hi.x - lo.x)) + 1e-30f;
+        float py = kBoxPadRel * (fmaxf(fabsf(lo.y), fabsf(hi.y)) + (hi.y - lo.y)) + 1e-30f;
+        float pz = kBoxPadRel * (fmaxf(fabsf(lo.z), fabsf(hi.z)) + (hi.z - lo.z)) + 1e-30f;
+        box.lx[i] = lo.x - px; box.ly[i] = lo.y - py; box.lz[i] = lo.z - pz;
+        box.hx[i] = hi.x + px; box.hy[i] = hi.y + py; box.hz[i] = hi.z + pz;
+        float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+        cent[i] = cx; cent[n + i] = cy; cent[2 * n + i] = cz;
+        c[0] = cmax[0] = cx; c[1] = cmax[1] = cy; c[2] = cmax[2] = cz;
+    }
+    // wave64 reductions, then one atomic per block and component
+    uint32_t v[6] = {f2ord(c[0]), f2ord(c[1]), f2ord(c[2]),
+                     f2ord(cmax[0]), f2ord(cmax[1]), f2ord(cmax[2])};
+    for (int off = 32; off > 0; off >>= 1) {
+        for (int k = 0; k < 3; ++k) v[k] = min(v[k], (uint32_t)__shfl_xor((int)v[k], off));
+        for (int k = 3; k < 6; ++k) v[k] = max(v[k], (uint32_t)__shfl_xor((int)v[k], off));
+    }
+    int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) red[k][wave] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        int k = threadIdx.x;
+        uint32_t r = red[k][0];
+        for (int w = 1; w < kBlock / 64; ++w) r = k < 3 ? min(r, red[k][w]) : max(r, red[k][w]);
+        if (k < 3) atomicMin(&cbounds[k], r);
+        else atomicMax(&cbounds[k], r);
+    }
+}
+
+__device__ __forceinline__ uint32_t expand10(uint32_t v)
+{
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_morton(const float* __restrict__ cent, int32_t n,
+                                                   const uint32_t* __restrict__ cbounds,
+                                                   uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float q[3];
+    for (int k = 0; k < 3; ++k) {
+        float lo = ord2f(cbounds[k]), hi = ord2f(cbounds[3 + k]);
+        float ext = hi - lo;
+        float x = ext > 0.0f ? (cent[k * n + i] - lo) / ext : 0.5f;
+        q[k] = fminf(fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+    }
+    keys[i] = (expand10((uint32_t)q[0]) << 2) | (expand10((uint32_t)q[1]) << 1) |
+              expand10((uint32_t)q[2]);
+    vals[i] = (uint32_t)i;
+}
+
+// ---------------------------------------------------------------- radix sort
+constexpr int kSortItems = 4;
+constexpr int kSortTile = kBlock * kSortItems;
+
+__global__ void __launch_bounds__(kBlock) k_sort_hist(const uint32_t* __restrict__ keys, int32_t n,
+                                                      int shift, int nblocks,
+                                                      uint32_t* __restrict__ hist)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    int base = blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortItems; ++r) {
+        int i = base + r * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];  // digit-major
+}
+
+// exclusive scan of m entries by one block of 1024 threads
+__global__ void __launch_bounds__(1024) k_scan_1block(uint32_t* __restrict__ a, int m)
+{
+    __shared__ uint32_t part[1024];
+    int per = (m + 1023) / 1024;
+    int b = threadIdx.x * per, e = min(b + per, m);
+    uint32_t s = 0;
+    for (int i = b; i < e; ++i) s += a[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;  // exclusive
+    for (int i = b; i < e; ++i) {
+        uint32_t x = a[i];
+        a[i] = run;
+        run += x;
+    }
+}
+
+// Stable scatter: keys of a tile are ranked in (round, thread) order; within a
+// wave, lanes with the same digit are found by 8 ballots (one per digit bit).
+__global__ void __launch_bounds__(kBlock) k_sort_scatter(const uint32_t* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin,
+                                                         uint32_t* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout, int32_t n,
+                                                         int shift, int nblocks,
+                                                         const uint32_t* __restrict__ offs)
+{
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[kBlock / 64][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    run[threadIdx.x] = offs[threadIdx.x * nblocks + blockIdx.x];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int base = blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortItems; ++r) {
+        for (int w = 0; w < kBlock / 64; ++w) wcnt[w][threadIdx.x] = 0;
+        __syncthreads();
+        int i = base + r * kBlock + threadIdx.x;
+        bool valid = i < n;
+        uint32_t key = valid ? kin[i] : 0u, val = valid ? vin[i] : 0u;
+        uint32_t dg = (key >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+        for (int bit = 0; bit < 8; ++bit) {
+            uint64_t bal = __ballot((dg >> bit) & 1u);
+            peers &= ((dg >> bit) & 1u) ? bal : ~bal;
+        }
+        uint32_t wrank = (uint32_t)__popcll(peers & lt);
+        if (valid && wrank == 0) wcnt[wave][dg] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[dg] + wrank;
+            for (int w = 0; w < wave; ++w) pos += wcnt[w][dg];
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+        for (int w = 0; w < kBlock / 64; ++w) add += wcnt[w][threadIdx.x];
+        run[threadIdx.x] += add;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- hierarchy
+__device__ __forceinline__ int delta(const uint32_t* __restrict__ keys, int32_t n, int i, int j)
+{
+    if (j < 0 || j > n - 1) return -1;
+    uint32_t a = keys[i], b = keys[j];
+    if (a == b) return 32 + __clz((int)((uint32_t)i ^ (uint32_t)j));
+    return __clz((int)(a ^ b));
+}
+
+// Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees and k-d
+// Trees" (HPG 2012), Fig. 4.  Children: >=0 internal, <0 leaf (~slot).
+__global__ void __launch_bounds__(kBlock) k_karras(const uint32_t* __restrict__ keys, int32_t n,
+                                                   int2* __restrict__ child,
+                                                   int32_t* __restrict__ parent_int,
+                                                   int32_t* __restrict__ parent_leaf)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n - 1) return;
+    int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
+    int dmin = delta(keys, n, i, i - d);
+    int lmax = 2;
+    while (delta(keys, n, i, i + lmax * d) > dmin) lmax *= 2;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+    int j = i + l * d;
+    int dnode = delta(keys, n, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    int gamma = i + s * d + min(d, 0);
+    int lo = min(i, j), hi = max(i, j);
+    int c0 = (lo == gamma) ? ~gamma : gamma;
+    int c1 = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
+    child[i] = make_int2(c0, c1);
+    if (c0 < 0) parent_leaf[~c0] = i; else parent_int[c0] = i;
+    if (c1 < 0) parent_leaf[~c1] = i; else parent_int[c1] = i;
+    if (i == 0) parent_int[0] = -1;
+}
+
+__global__ void __launch_bounds__(kBlock) k_depth(const int32_t* __restrict__ parent_int,
+                                                  int32_t m, int32_t* __restrict__ depth,
+                                                  int32_t* __restrict__ max_depth)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    int dd = 0;
+    for (int p = i; p > 0 && dd < 4096; p = parent_int[p]) ++dd;
+    depth[i] = dd;
+    atomicMax(max_depth, dd);
+}
+
+__device__ __forceinline__ void child_box(int c, const Soa6& leaf, const uint32_t* __restrict__ vals,
+                                          const Soa6& ib, float b[6])
+{
+    if (c < 0) {
+        int o = (int)vals[~c];
+        b[0] = leaf.lx[o]; b[1] = leaf.ly[o]; b[2] = leaf.lz[o];
+        b[3] = leaf.hx[o]; b[4] = leaf.hy[o]; b[5] = leaf.hz[o];
+    } else {
+        b[0] = ib.lx[c]; b[1] = ib.ly[c]; b[2] = ib.lz[c];
+        b[3] = ib.hx[c]; b[4] = ib.hy[c]; b[5] = ib.hz[c];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_refit_level(const int2* __restrict__ child,
+                                                        const int32_t* __restrict__ depth,
+                                                        int32_t m, int level, Soa6 leaf,
+                                                        const uint32_t* __restrict__ vals, Soa6 ib)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m || depth[i] != level) return;
+    int2 c = child[i];
+    float a[6], b[6];
+    child_box(c.x, leaf, vals, ib, a);
+    child_box(c.y, leaf, vals, ib, b);
+    ib.lx[i] = fminf(a[0], b[0]); ib.ly[i] = fminf(a[1], b[1]); ib.lz[i] = fminf(a[2], b[2]);
+    ib.hx[i] = fmaxf(a[3], b[3]); ib.hy[i] = fmaxf(a[4], b[4]); ib.hz[i] = fmaxf(a[5], b[5]);
+}
+
+__global__ void __launch_bounds__(kBlock) k_assemble(const int2* __restrict__ child,
+                                                     const int32_t* __restrict__ depth, int32_t m,
+                                                     Soa6 leaf, const uint32_t* __restrict__ vals,
+                                                     Soa6 ib, BvhNode* __restrict__ nodes)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    int2 c = child[i];
+    float a[6], b[6];
+    child_box(c.x, leaf, vals, ib, a);
+    child_box(c.y, leaf, vals, ib, b);
+    nodes[i].a = f4(a[0], a[1], a[2], a[3]);
+    nodes[i].b = f4(a[4], a[5], b[0], b[1]);
+    nodes[i].c = f4(b[2], b[3], b[4], b[5]);
+    nodes[i].d = make_int4(c.x, c.y, depth[i], 0);
+}
+
+__global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tris9, int32_t n,
+                                                    const uint32_t* __restrict__ vals,
+                                                    TriPre* __restrict__ pre)
+{
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= n) return;
+    int o = (int)vals[k];
+    const float* t = tris9 + 9 * (int64_t)o;
+    f3 v0 = mk(t[0], t[1], t[2]), v1 = mk(t[3], t[4], t[5]), v2 = mk(t[6], t[7], t[8]);
+    f3 e1 = v1 - v0, e2 = v2 - v0;  // maths.cpp:341-342, same roundings
+    pre[k].a = f4(v0.x, v0.y, v0.z, e1.x);
+    pre[k].b = f4(e1.y, e1.z, e2.x, e2.y);
+    pre[k].c = f4(e2.z, __int_as_float(o), 0.0f, 0.0f);
+}
+
+// single-triangle scene: one node whose two children are the same leaf
+__global__ void k_single(Soa6 leaf, BvhNode* nodes)
+{
+    nodes[0].a = f4(leaf.lx[0], leaf.ly[0], leaf.lz[0], leaf.hx[0]);
+    nodes[0].b = f4(leaf.hy[0], leaf.hz[0], leaf.lx[0], leaf.ly[0]);
+    nodes[0].c = f4(leaf.lz[0], leaf.hx[0], leaf.hy[0], leaf.hz[0]);
+    nodes[0].d = make_int4(~0, ~0, 0, 0);
+}
+
+inline int blocks_for(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+}  // namespace
+
+int build_lbvh(Scene& s, const float* d_tris9)
+{
+    const int32_t n = s.n;
+    hipStream_t st = s.stream;
+    auto t0 = std::chrono::steady_clock::now();
+    const int32_t m = n >= 2 ? n - 1 : 1;  // internal nodes
+    s.n_nodes = m;
+    TMPT_HIP(hipMalloc(&s.nodes, sizeof(BvhNode) * (size_t)m));
+    TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * (size_t)std::max(n, 1)));
+    TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(n, 1)));
+    if (n == 0) {
+        TMPT_HIP(hipMemsetAsync(s.nodes, 0, sizeof(BvhNode), st));
+        s.max_depth = 0;
+        return 0;
+    }
+    // scratch
+    const int nb_sort = blocks_for(n, kSortTile);
+    size_t nn = (size_t)n;
+    std::vector<void*> tmp;
+    auto alloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        tmp.push_back(p);
+        return p;
+    };
+    auto free_all = [&]() {
+        for (void* p : tmp) (void)hipFree(p);
+        tmp.clear();
+    };
+    float* leafbuf = (float*)alloc(6 * nn * sizeof(float));
+    float* ibbuf = (float*)alloc(6 * (size_t)m * sizeof(float));
+    float* cent = (float*)alloc(3 * nn * sizeof(float));
+    uint32_t* cb = (uint32_t*)alloc(6 * sizeof(uint32_t));
+    uint32_t* k0 = (uint32_t*)alloc(nn * 4);
+    uint32_t* v0 = (uint32_t*)alloc(nn * 4);
+    uint32_t* k1 = (uint32_t*)alloc(nn * 4);
+    uint32_t* v1 = (uint32_t*)alloc(nn * 4);
+    uint32_t* hist = (uint32_t*)alloc((size_t)256 * nb_sort * 4);
+    int2* child = (int2*)alloc((size_t)m * sizeof(int2));
+    int32_t* pint = (int32_t*)alloc((size_t)m * 4);
+    int32_t* pleaf = (int32_t*)alloc(nn * 4);
+    int32_t* depth = (int32_t*)alloc((size_t)m * 4);
+    int32_t* maxd = (int32_t*)alloc(4);
+    if (!leafbuf || !ibbuf || !cent || !cb || !k0 || !v0 || !k1 || !v1 || !hist || !child ||
+        !pint || !pleaf || !depth || !maxd) {
+        free_all();
+        set_error("build_lbvh: out of device memory");
+        return -1;
+    }
+    Soa6 leaf{leafbuf, leafbuf + nn, leafbuf + 2 * nn, leafbuf + 3 * nn, leafbuf + 4 * nn,
+              leafbuf + 5 * nn};
+    size_t mm = (size_t)m;
+    Soa6 ib{ibbuf, ibbuf + mm, ibbuf + 2 * mm, ibbuf + 3 * mm, ibbuf + 4 * mm, ibbuf + 5 * mm};
+    uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+    int rc = 0;
+    do {
+        if (hipMemcpyAsync(cb, init, sizeof(init), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
+        if (hipMemsetAsync(maxd, 0, 4, st) != hipSuccess) { rc = -1; break; }
+        k_tri_prep<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, s.tri_orig, leaf, cent, cb);
+        k_morton<<<blocks_for(n, kBlock), kBlock, 0, st>>>(cent, n, cb, k0, v0);
+        uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+        for (int pass = 0; pass < 4; ++pass) {
+            k_sort_hist<<<nb_sort, kBlock, 0, st>>>(ki, n, 8 * pass, nb_sort, hist);
+            k_scan_1block<<<1, 1024, 0, st>>>(hist, 256 * nb_sort);
+            k_sort_scatter<<<nb_sort, kBlock, 0, st>>>(ki, vi, ko, vo, n, 8 * pass, nb_sort, hist);
+            std::swap(ki, ko);
+            std::swap(vi, vo);
+        }
+        // sorted (ki, vi)
+        k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, vi, s.tri_pre);
+        if (n == 1) {
+            k_single<<<1, 1, 0, st>>>(leaf, s.nodes);
+            s.max_depth = 0;
+            break;
+        }
+        k_karras<<<blocks_for(m, kBlock), kBlock, 0, st>>>(ki, n, child, pint, pleaf);
+        k_depth<<<blocks_for(m, kBlock), kBlock, 0, st>>>(pint, m, depth, maxd);
+        int32_t hmax = 0;
+        if (hipMemcpyAsync(&hmax, maxd, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }
+        s.max_depth = hmax;
+        if (hmax + 2 > kStackTotal) {
+            set_error("build_lbvh: tree depth " + std::to_string(hmax) + " exceeds the traversal stack");
+            rc = -2;
+            break;
+        }
+        for (int L = hmax; L >= 0; --L)
+            k_refit_level<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, L, leaf, vi, ib);
+        k_assemble<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, leaf, vi, ib, s.nodes);
+    } while (0);
+    hipError_t e = hipGetLastError();
+    hipError_t e2 = hipStreamSynchronize(st);
+    free_all();
+    if (rc == -1 || e != hipSuccess || e2 != hipSuccess) {
+        set_error(std::string("build_lbvh: ") + hipGetErrorString(e != hipSuccess ? e : e2));
+        return -1;
+    }
+    if (rc) return rc;
+    s.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+// ---------------------------------------------------------------- sin/cos table
+// (cos a, sin a) for all 2^24 RNG keys of RandomUnitVector (maths.cpp:33-36),
+// computed by the host's libm so the device reproduces it exactly.
+const float2* device_sincos_table(int device)
+{
+    static std::mutex mu;
+    static std::vector<float2*> tables;
+    static std::vector<float2> host;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)tables.size() <= device) tables.resize(device + 1, nullptr);
+    if (tables[device]) return tables[device];
+    const size_t N = size_t(1) << 24;
+    if (host.empty()) {
+        host.resize(N);
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([t, nt]() {
+                size_t b = N * t / nt, e = N * (t + 1) / nt;
+                for (size_t k = b; k < e; ++k) {
+                    float a = unit_angle((uint32_t)k);
+                    host[k] = make_float2(cosf(a), sinf(a));
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    float2* d = nullptr;
+    if (hipMalloc(&d, N * sizeof(float2)) != hipSuccess) {
+        set_error("sincos table: hipMalloc failed");
+        return nullptr;
+    }
+    if (hipMemcpy(d, host.data(), N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        set_error("sincos table: upload failed");
+        return nullptr;
+    }
+    tables[device] = d;
+    return d;
+}
+
+}  // namespace tmpt

@@ -1,0 +1,112 @@
+// tmpt_cli.cpp -- the reference's command line (main.cpp:248-345) over the C ABI:
+//   tmpt <width> <height> <spp> <objFile> [--seed row|pixel] [--engine wavefront|mega]
+//        [--gpus N] [--device D] [--out output.png]
+// Defaults reproduce the reference: row seeding (main.cpp:204) and output.png.
+// Pixel seeding is what the wavefront engine parallelises; row mode runs the
+// megakernel (one lane per row).  With --gpus N the rows are dealt to N
+// devices in 16-row bands, one host thread per device, and assembled here.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tmpt.h"
+
+static double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, const char** argv)
+{
+    if (argc < 5) {
+        printf("Usage: tmpt [width] [height] [samplesPerPixel] [objFile] [--seed row|pixel] "
+               "[--engine wavefront|mega] [--gpus N] [--device D] [--out file.png]\n");
+        return 1;
+    }
+    int w = atoi(argv[1]);
+    if (w < 1 || w > 10000) { printf("ERROR: invalid width argument '%s'\n", argv[1]); return 1; }
+    int h = atoi(argv[2]);
+    if (h < 1 || h > 10000) { printf("ERROR: invalid height argument '%s'\n", argv[2]); return 1; }
+    int spp = atoi(argv[3]);
+    if (spp < 1 || spp > 1024) { printf("ERROR: invalid samplesPerPixel argument '%s'\n", argv[3]); return 1; }
+    const char* obj = argv[4];
+    int seed = TMPT_SEED_ROW, engine = TMPT_ENGINE_WAVEFRONT, gpus = 1, device = 0;
+    const char* out = "output.png";
+    for (int i = 5; i < argc; ++i) {
+        if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strcmp(argv[++i], "pixel") ? TMPT_SEED_ROW : TMPT_SEED_PIXEL;
+        else if (!strcmp(argv[i], "--engine") && i + 1 < argc) engine = strcmp(argv[++i], "mega") ? TMPT_ENGINE_WAVEFRONT : TMPT_ENGINE_MEGAKERNEL;
+        else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--out") && i + 1 < argc) out = argv[++i];
+        else { printf("ERROR: unknown option '%s'\n", argv[i]); return 1; }
+    }
+    float* tris = nullptr;
+    int32_t n = 0;
+    float bmin[3], bmax[3];
+    if (tmpt_load_obj(obj, &tris, &n, bmin, bmax)) {
+        printf("ERROR: failed to load .obj file\n");
+        return 1;
+    }
+    int ndev = tmpt_device_count();
+    if (gpus < 1) gpus = 1;
+    if (device + gpus > ndev) {
+        printf("ERROR: %d GPU(s) requested from device %d, %d present\n", gpus, device, ndev);
+        return 1;
+    }
+    tmpt_camera cam;
+    tmpt_camera_for_scene(&cam, bmin, bmax, w, h, strstr(obj, "sponza.obj") != nullptr);
+
+    std::vector<tmpt_scene*> scenes(gpus, nullptr);
+    std::vector<int> rcs(gpus, 0);
+    double t0 = now_s();
+    {
+        std::vector<std::thread> th;
+        for (int g = 0; g < gpus; ++g)
+            th.emplace_back([&, g]() { rcs[g] = tmpt_scene_create(tris, n, device + g, &scenes[g]); });
+        for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < gpus; ++g)
+        if (rcs[g]) { printf("ERROR: scene init failed: %s\n", tmpt_last_error()); return 1; }
+    printf("Initialized scene '%s' (%i tris) in %.3fs\n", obj, n, now_s() - t0);
+
+    std::vector<uint8_t> image((size_t)w * h * 4, 0);
+    std::vector<std::vector<uint8_t>> tiles(gpus);
+    std::vector<uint64_t> rays(gpus, 0);
+    std::vector<tmpt_render_desc> desc(gpus);
+    for (int g = 0; g < gpus; ++g) {
+        memset(&desc[g], 0, sizeof(tmpt_render_desc));
+        desc[g].width = w; desc[g].height = h; desc[g].spp = spp; desc[g].seed_mode = seed;
+        desc[g].band_rows = gpus > 1 ? 16 : 0; desc[g].shard = g; desc[g].num_shards = gpus;
+        desc[g].engine = engine;
+        tiles[g].resize((size_t)tmpt_tile_rows(&desc[g]) * w * 4);
+    }
+    t0 = now_s();
+    {
+        std::vector<std::thread> th;
+        for (int g = 0; g < gpus; ++g)
+            th.emplace_back([&, g]() { rcs[g] = tmpt_render(scenes[g], &cam, &desc[g], tiles[g].data(), &rays[g]); });
+        for (auto& t : th) t.join();
+    }
+    const double dt = now_s() - t0;
+    uint64_t total = 0;
+    for (int g = 0; g < gpus; ++g) {
+        if (rcs[g]) { printf("ERROR: render failed: %s\n", tmpt_last_error()); return 1; }
+        total += rays[g];
+        int rows = tmpt_tile_rows(&desc[g]);
+        for (int r = 0; r < rows; ++r) {
+            int y = tmpt_tile_row_to_y(&desc[g], r);
+            memcpy(&image[(size_t)y * w * 4], &tiles[g][(size_t)r * w * 4], (size_t)w * 4);
+        }
+    }
+    printf("Rendered scene at %ix%i,%ispp in %.3f s\n", w, h, spp, dt);
+    printf("- %.1f K Rays, %.1f K Rays/s\n", total / 1000.0, total / 1000.0 / dt);
+    if (tmpt_write_png(out, image.data(), w, h)) { printf("ERROR: %s\n", tmpt_last_error()); return 1; }
+    for (auto* s : scenes) tmpt_scene_destroy(s);
+    tmpt_free(tris);
+    return 0;
+}

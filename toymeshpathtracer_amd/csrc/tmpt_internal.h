@@ -1,0 +1,99 @@
+// tmpt_internal.h -- device data layout and the scene object behind the C ABI.
+//
+// HBM layout of one scene (DESIGN.md "Data layout in HBM"):
+//   nodes    BvhNode[max(n-1,1)]  64 B  LBVH2 internal nodes; each holds BOTH
+//                                        child boxes, so one node visit is one
+//                                        128-B line (4 x dwordx4 loads)
+//   tri_pre  TriPre[n]            48 B  leaf order: v0, e1 = v1-v0, e2 = v2-v0,
+//                                        original index (the Moller-Trumbore operands)
+//   tri_orig TriOrig[n]           48 B  original order: v0, v1, v2 and the geometric
+//                                        normal, read once per accepted hit
+//   sincos   float2[2^24]        128 MB (cos a, sin a) of RandomUnitVector's angle,
+//                                        filled from the host libm (shared per device)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "tmpt_math.h"
+
+namespace tmpt {
+
+struct alignas(16) BvhNode {
+    float4 a;  // c0.min.xyz, c0.max.x
+    float4 b;  // c0.max.yz,  c1.min.xy
+    float4 c;  // c1.min.z,   c1.max.xyz
+    int4 d;    // child0, child1 (>=0 internal node, <0 leaf = ~triangle slot), depth, 0
+};
+static_assert(sizeof(BvhNode) == 64, "node is one half cache line");
+
+struct alignas(16) TriPre {
+    float4 a;  // v0.xyz, e1.x
+    float4 b;  // e1.yz, e2.xy
+    float4 c;  // e2.z, original index (int bits), 0, 0
+};
+struct alignas(16) TriOrig {
+    float4 a;  // v0.xyz, v1.x
+    float4 b;  // v1.yz, v2.xy
+    float4 c;  // v2.z, normal.xyz
+};
+
+// Box culling is conservative (DESIGN.md "Scene query contract"): leaf boxes are
+// inflated by kBoxPadRel * (|coord| + extent) and the far slab distance is
+// stretched by kTfarSlack, so every triangle the reference would accept is
+// reached and Moller-Trumbore alone decides.
+constexpr float kBoxPadRel = 1e-5f;
+constexpr float kTfarSlack = 1.00001f;
+
+// Stack: kStackLds entries per lane live in LDS, the rest spill to a global
+// per-lane area.  An LBVH over (30-bit Morton, index) keys has depth <= 62, so
+// kStackTotal = 64 always suffices (DESIGN.md "Traversal").
+constexpr int kStackTotal = 64;
+
+struct Scene {
+    int device = 0;
+    int32_t n = 0;          // triangles incl. the floor
+    int32_t n_nodes = 0;    // internal nodes
+    int32_t max_depth = 0;  // of the LBVH
+    BvhNode* nodes = nullptr;
+    TriPre* tri_pre = nullptr;
+    TriOrig* tri_orig = nullptr;
+    const float2* sincos = nullptr;  // borrowed from the per-device table
+    hipStream_t stream = nullptr;
+    double build_ms = 0.0;
+    // render workspace (grown on demand, reused across calls)
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    // statistics of the last render
+    double render_ms = 0.0;
+    double extend_ms = 0.0;
+    double shadow_ms = 0.0;
+    uint64_t extend_rays = 0, shadow_rays = 0;
+    int64_t extend_launches = 0, shadow_launches = 0, iterations = 0;
+    uint64_t node_visits = 0, tri_tests = 0;  // only with TMPT_FLAG_COUNT_VISITS
+    uint64_t shadow_node_visits = 0, shadow_tri_tests = 0;
+};
+
+// error plumbing: last error is thread-local, ints cross the ABI, never exceptions
+void set_error(const std::string& msg);
+const char* last_error();
+
+#define TMPT_HIP(call)                                                                  \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ::tmpt::set_error(std::string(#call) + ": " + hipGetErrorString(e_));       \
+            return -1;                                                                  \
+        }                                                                               \
+    } while (0)
+
+// tmpt_bvh.hip
+int build_lbvh(Scene& s, const float* d_tris9);
+// sincos table for the current device (created on first use, never freed)
+const float2* device_sincos_table(int device);
+
+TMPT_HD float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+
+}  // namespace tmpt

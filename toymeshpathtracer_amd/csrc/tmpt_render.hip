@@ -1,0 +1,631 @@
+// tmpt_render.hip -- the path tracer of main.cpp:44-119 / 172-246 on gfx950.
+//
+// Engines (DESIGN.md "Kernels"):
+//  * wavefront (pixel mode): per-pixel path state in HBM (SoA), one slot per
+//    pixel of the tile; every iteration runs
+//        extend  closest-hit traversal of the active queue     (persistent waves)
+//        shade   hit -> shadow ray + next bounce; miss/max depth -> backward
+//                recurrence, accumulate, next camera sample or pixel write
+//        shadow  any-hit traversal of the shadow queue          (persistent waves)
+//    queues are compacted with wave64 ballot + mbcnt prefix and ONE atomic per
+//    wave.  Samples of a pixel stay sequential (its RNG stream threads through
+//    them, main.cpp:204-218), so parallelism is over pixels.
+//  * megakernel: one lane per pixel (pixel mode) or per row (row mode: the
+//    unmodified reference RNG chain, H-way parallel -- a correctness mode).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "tmpt.h"
+#include "tmpt_internal.h"
+#include "tmpt_traverse.h"
+
+namespace tmpt {
+
+struct RenderArgs {
+    Camera cam;
+    int32_t W, H, spp, seed_mode, band_rows, shard, nshards, tile_rows;
+    float invW, invH, spp_recip;
+    int64_t slots;  // tile_rows * W
+};
+
+__device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
+{
+    int lb = lr / a.band_rows, r = lr - lb * a.band_rows;
+    return (lb * a.nshards + a.shard) * a.band_rows + r;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// wave64 sum of a 32-bit value (all lanes must call)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+
+// Compacted append: every lane of the wave calls; lanes with pred get
+// consecutive slots, one atomic per wave (ballot + mbcnt prefix).
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred)
+{
+    uint64_t m = __ballot(pred);
+    if (m == 0) return 0;
+    int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return base + below;
+}
+
+template <int BLOCK, bool COUNT>
+__device__ __forceinline__ void flush_counts(unsigned long long* counters, uint32_t rays,
+                                             const TravCount& cnt)
+{
+    uint32_t r = wave_sum(rays);
+    uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
+    uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
+    if (lane_id() == 0) {
+        atomicAdd(&counters[0], (unsigned long long)r);
+        if (COUNT) {
+            atomicAdd(&counters[1], (unsigned long long)nv);
+            atomicAdd(&counters[2], (unsigned long long)nt);
+        }
+    }
+}
+
+// ============================================================ megakernel
+template <bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
+                                         uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
+                                         TravCount& cnt)
+{
+    int depth = 0;
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
+        ++rays;
+        float t, u, v;
+        int id = traverse<false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+        if (id >= 0) {
+            f3 pos, nrm;
+            hit_record(sv, id, u, v, pos, nrm);
+            ++rays;  // shadow ray, main.cpp:57-59
+            float ts, us, vs;
+            int sid = traverse<true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT, ts,
+                                            us, vs, st, cnt);
+            lbuf[depth * BLOCK] = sid >= 0 ? 0.0f : light_cosine(nrm, d);
+            f3 rnd = random_unit_vector(rng, sv.sincos);  // main.cpp:71-72
+            f3 target = pos + nrm + rnd;
+            d = normalize(target - pos);
+            o = pos;
+            ++depth;
+        } else {
+            color = sky(d);
+            break;
+        }
+    }
+    for (int i = depth - 1; i >= 0; --i) color = backward_step(color, lbuf[i * BLOCK]);
+    return color;
+}
+
+template <bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const RenderArgs& a, int x,
+                                                 int y, uint32_t& rng, uint32_t& rays,
+                                                 TravStack<BLOCK, SL>& st, float* lbuf,
+                                                 TravCount& cnt)
+{
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    for (int s = 0; s < a.spp; ++s) {  // main.cpp:209-219
+        f3 o, d;
+        camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
+        col = col + trace_path<COUNT>(sv, o, d, rng, rays, st, lbuf, cnt);
+    }
+    return pack_pixel(col, a.spp_recip);
+}
+
+template <bool ROW, bool COUNT, int BLOCK, int SL>
+__global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
+                                                uint32_t* __restrict__ out,
+                                                uint32_t* __restrict__ ovf,
+                                                unsigned long long* __restrict__ counters)
+{
+    __shared__ uint32_t s_stack[SL * BLOCK];
+    __shared__ float s_light[kMaxDepth * BLOCK];
+    const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    float* lbuf = &s_light[threadIdx.x];
+    uint32_t rays = 0;
+    TravCount cnt;
+    const int64_t items = ROW ? (int64_t)a.tile_rows : a.slots;
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t w = gtid; w < items; w += stride) {
+        if (ROW) {
+            int lr = (int)w;
+            int y = tile_row_to_y(a, lr);
+            uint32_t rng = row_seed((uint32_t)y);  // main.cpp:204, unmodified
+            for (int x = 0; x < a.W; ++x)
+                out[(int64_t)lr * a.W + x] = render_pixel<COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+        } else {
+            int lr = (int)(w / a.W), x = (int)(w - (int64_t)lr * a.W);
+            int y = tile_row_to_y(a, lr);
+            uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)a.W);
+            out[w] = render_pixel<COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+        }
+    }
+    flush_counts<BLOCK, COUNT>(counters, rays, cnt);
+}
+
+// ============================================================ batched HitScene
+template <bool ANY, int BLOCK, int SL>
+__global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* __restrict__ rays,
+                                                     int64_t n, float tmin, float tmax,
+                                                     float* __restrict__ hits,
+                                                     int32_t* __restrict__ ids,
+                                                     uint32_t* __restrict__ ovf)
+{
+    __shared__ uint32_t s_stack[SL * BLOCK];
+    const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    TravCount cnt;
+    for (int64_t i = gtid; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        const float* r = rays + 6 * i;
+        f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+        float t, u, v;
+        int id = traverse<ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
+        ids[i] = id;
+        if (id >= 0) {
+            f3 pos, nrm;
+            hit_record(sv, id, u, v, pos, nrm);
+            float* h = hits + 7 * i;
+            h[0] = pos.x; h[1] = pos.y; h[2] = pos.z;
+            h[3] = nrm.x; h[4] = nrm.y; h[5] = nrm.z;
+            h[6] = t;
+        }
+    }
+}
+
+// ============================================================ wavefront
+struct WfState {
+    uint32_t* rng;
+    uint32_t* smp;
+    uint32_t* depth;
+    float* col;    // [3][P]
+    float* light;  // [kMaxDepth][P]
+    float* ray;    // [6][P]  o.xyz d.xyz
+    float* hit;    // [3][P]  t u v
+    int32_t* hid;  // [P]
+    float* sho;    // [3][P] shadow origin
+    uint32_t* q[2];
+    uint32_t* qs;
+    uint32_t* ctl;  // control words, see kCtl*
+    unsigned long long* tot;  // [0] extend rays [1] shadow rays [2,3] extend node/tri visits [4,5] shadow
+    int64_t P;
+};
+// control words (uint32): queue counts per parity, shadow count, fetch heads
+enum { kCtlCount0 = 0, kCtlCount1 = 1, kCtlShadow = 2, kCtlHeadE = 3, kCtlHeadS = 4, kCtlWords = 16 };
+
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
+{
+    int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= s.P) return;
+    int lr = (int)(p / a.W), x = (int)(p - (int64_t)lr * a.W);
+    int y = tile_row_to_y(a, lr);
+    uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)a.W);
+    f3 o, d;
+    camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
+    const int64_t P = s.P;
+    s.rng[p] = rng;
+    s.smp[p] = 0;
+    s.depth[p] = 0;
+    s.col[p] = 0.0f; s.col[P + p] = 0.0f; s.col[2 * P + p] = 0.0f;
+    s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
+    s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
+    s.q[0][p] = (uint32_t)p;
+}
+
+// Persistent traversal over a queue: each wave takes 64 queue entries at a
+// time from a fetch head (one atomic per wave) until the queue is drained.
+template <bool ANY, bool COUNT, int BLOCK, int SL>
+__global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int parity,
+                                                    uint32_t* __restrict__ ovf)
+{
+    __shared__ uint32_t s_stack[SL * BLOCK];
+    const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    TravCount cnt;
+    uint32_t traced = 0;
+    const uint32_t* q = ANY ? s.qs : s.q[parity];
+    const uint32_t n = ANY ? s.ctl[kCtlShadow] : s.ctl[kCtlCount0 + parity];
+    uint32_t* head = &s.ctl[ANY ? kCtlHeadS : kCtlHeadE];
+    const int64_t P = s.P;
+    const f3 ldir = light_dir();
+    for (;;) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(head, 64u);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        uint32_t i = base + (uint32_t)lane_id();
+        if (i < n) {
+            uint32_t p = q[i];
+            if (ANY) {
+                f3 o = mk(s.sho[p], s.sho[P + p], s.sho[2 * P + p]);
+                float t, u, v;
+                int id = traverse<true, COUNT>(sv, make_trav_ray(o, ldir), kMinT, kMaxT, t, u, v, st, cnt);
+                ++traced;
+                if (id >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
+            } else if (s.depth[p] < (uint32_t)kMaxDepth) {
+                f3 o = mk(s.ray[p], s.ray[P + p], s.ray[2 * P + p]);
+                f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
+                float t, u = 0.0f, v = 0.0f;
+                int id = traverse<false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+                ++traced;
+                s.hid[p] = id;
+                s.hit[P + p] = u;
+                s.hit[2 * P + p] = v;
+            }
+        }
+    }
+    uint32_t r = wave_sum(traced);
+    uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
+    uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
+    if (lane_id() == 0) {
+        atomicAdd(&s.tot[ANY ? 1 : 0], (unsigned long long)r);
+        if (COUNT) {
+            atomicAdd(&s.tot[ANY ? 4 : 2], (unsigned long long)nv);
+            atomicAdd(&s.tot[ANY ? 5 : 3], (unsigned long long)nt);
+        }
+    }
+}
+
+// shade: consumes the extend queue of `parity`, appends to the other parity's
+// queue and to the shadow queue; writes finished pixels.
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, WfState s,
+                                                    int parity, uint32_t* __restrict__ out)
+{
+    const uint32_t n = s.ctl[kCtlCount0 + parity];
+    uint32_t* qn = s.q[parity ^ 1];
+    const int64_t P = s.P;
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    // all lanes iterate the same number of times (wave-uniform appends)
+    const int64_t iters = ((int64_t)n + stride - 1) / stride;
+    for (int64_t it = 0; it < iters; ++it) {
+        int64_t i = it * stride + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+        bool valid = i < (int64_t)n;
+        bool cont = false, shadow = false;
+        uint32_t p = valid ? s.q[parity][i] : 0u;
+        if (valid) {
+            uint32_t depth = s.depth[p];
+            uint32_t rng = s.rng[p];
+            f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
+            int id = depth < (uint32_t)kMaxDepth ? s.hid[p] : -1;
+            bool finish = true;
+            f3 color = mk(0.0f, 0.0f, 0.0f);
+            if (depth < (uint32_t)kMaxDepth) {
+                if (id >= 0) {  // Scatter, main.cpp:44-73
+                    f3 pos, nrm;
+                    hit_record(sv, id, s.hit[P + p], s.hit[2 * P + p], pos, nrm);
+                    s.light[(int64_t)depth * P + p] = light_cosine(nrm, d);  // zeroed by shadow if occluded
+                    s.sho[p] = pos.x; s.sho[P + p] = pos.y; s.sho[2 * P + p] = pos.z;
+                    f3 rnd = random_unit_vector(rng, sv.sincos);
+                    f3 target = pos + nrm + rnd;
+                    d = normalize(target - pos);
+                    s.ray[p] = pos.x; s.ray[P + p] = pos.y; s.ray[2 * P + p] = pos.z;
+                    s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
+                    ++depth;
+                    shadow = true;
+                    cont = true;  // depth == kMaxDepth: finished next iteration, after its shadow
+                    finish = false;
+                } else {
+                    color = sky(d);  // main.cpp:106-107
+                }
+            }
+            if (finish) {
+                for (int k = (int)depth - 1; k >= 0; --k)
+                    color = backward_step(color, s.light[(int64_t)k * P + p]);
+                f3 col = mk(s.col[p], s.col[P + p], s.col[2 * P + p]) + color;
+                uint32_t smp = s.smp[p] + 1;
+                s.smp[p] = smp;
+                depth = 0;
+                if (smp < (uint32_t)a.spp) {
+                    s.col[p] = col.x; s.col[P + p] = col.y; s.col[2 * P + p] = col.z;
+                    int lr = (int)(p / (uint32_t)a.W), x = (int)(p - (uint32_t)lr * (uint32_t)a.W);
+                    int y = tile_row_to_y(a, lr);
+                    f3 o;
+                    camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
+                    s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
+                    s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
+                    cont = true;
+                } else {
+                    out[p] = pack_pixel(col, a.spp_recip);
+                }
+            }
+            s.depth[p] = depth;
+            s.rng[p] = rng;
+        }
+        uint32_t qi = wave_append(&s.ctl[kCtlCount0 + (parity ^ 1)], cont);
+        if (cont) qn[qi] = p;
+        uint32_t si = wave_append(&s.ctl[kCtlShadow], shadow);
+        if (shadow) s.qs[si] = p;
+    }
+}
+
+// between iterations: retire the consumed queue, reset fetch heads
+__global__ void k_wf_advance(WfState s, int parity)
+{
+    s.ctl[kCtlCount0 + parity] = 0;
+    s.ctl[kCtlHeadE] = 0;
+    s.ctl[kCtlHeadS] = 0;
+    s.ctl[kCtlShadow] = 0;
+}
+
+// ============================================================ host side
+namespace {
+
+constexpr int kBlk = 256;
+constexpr int kSL = 32;  // LDS stack entries per lane
+
+int occupancy_grid(const void* fn, int block, size_t dyn_lds, int device)
+{
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, dyn_lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        cus < 1)
+        cus = 256;
+    return per_cu * cus;
+}
+
+int ensure_ws(Scene& s, size_t bytes)
+{
+    if (s.ws_bytes >= bytes) return 0;
+    if (s.ws) (void)hipFree(s.ws);
+    s.ws = nullptr;
+    s.ws_bytes = 0;
+    TMPT_HIP(hipMalloc(&s.ws, bytes));
+    s.ws_bytes = bytes;
+    return 0;
+}
+
+SceneView view(const Scene& s)
+{
+    return SceneView{s.nodes, s.tri_pre, s.tri_orig, s.sincos, s.n};
+}
+
+RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
+{
+    RenderArgs a;
+    a.cam.origin = mk(c->origin[0], c->origin[1], c->origin[2]);
+    a.cam.lower_left = mk(c->lower_left[0], c->lower_left[1], c->lower_left[2]);
+    a.cam.horizontal = mk(c->horizontal[0], c->horizontal[1], c->horizontal[2]);
+    a.cam.vertical = mk(c->vertical[0], c->vertical[1], c->vertical[2]);
+    a.cam.u = mk(c->u[0], c->u[1], c->u[2]);
+    a.cam.v = mk(c->v[0], c->v[1], c->v[2]);
+    a.cam.w = mk(c->w[0], c->w[1], c->w[2]);
+    a.cam.lens_radius = c->lens_radius;
+    a.W = d->width;
+    a.H = d->height;
+    a.spp = d->spp;
+    a.seed_mode = d->seed_mode;
+    a.band_rows = d->band_rows > 0 ? d->band_rows : d->height;
+    a.shard = d->num_shards > 1 ? d->shard : 0;
+    a.nshards = d->num_shards > 1 ? d->num_shards : 1;
+    a.tile_rows = tmpt_tile_rows(d);
+    a.invW = 1.0f / (float)d->width;             // main.cpp:186
+    a.invH = 1.0f / (float)d->height;            // main.cpp:187
+    a.spp_recip = 1.0f / (float)d->spp;          // main.cpp:188
+    a.slots = (int64_t)a.tile_rows * a.W;
+    return a;
+}
+
+template <bool ROW, bool COUNT>
+int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long* counters)
+{
+    auto fn = k_mega<ROW, COUNT, kBlk, kSL>;
+    int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    int64_t items = ROW ? a.tile_rows : a.slots;
+    grid = (int)std::min<int64_t>(grid, (items + kBlk - 1) / kBlk);
+    grid = std::max(grid, 1);
+    size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);
+    if (ensure_ws(s, ovf_bytes)) return -1;
+    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, out, (uint32_t*)s.ws, counters);
+    TMPT_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+
+int render_megakernel(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
+                      unsigned long long* d_counters)
+{
+    bool row = a.seed_mode == TMPT_SEED_ROW;
+    if (row) return count ? launch_mega<true, true>(s, a, d_out, d_counters)
+                          : launch_mega<true, false>(s, a, d_out, d_counters);
+    return count ? launch_mega<false, true>(s, a, d_out, d_counters)
+                 : launch_mega<false, false>(s, a, d_out, d_counters);
+}
+
+// Wavefront driver.  The host enqueues iterations without reading the queue
+// sizes (the kernels read them from device memory) and checks for completion
+// every kCheck iterations.
+int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
+{
+    const int64_t P = a.slots;
+    const size_t Pz = (size_t)P;
+    auto trace_e = count ? k_wf_trace<false, true, kBlk, kSL> : k_wf_trace<false, false, kBlk, kSL>;
+    auto trace_s = count ? k_wf_trace<true, true, kBlk, kSL> : k_wf_trace<true, false, kBlk, kSL>;
+    int grid_t = occupancy_grid((const void*)trace_e, kBlk, 0, s.device);
+    int grid_sh = 0, cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device);
+    grid_sh = cus * 8;
+    size_t ovf_words = (size_t)grid_t * kBlk * (kStackTotal - kSL);
+    // layout of the workspace
+    size_t words = 0;
+    auto take = [&](size_t w) { size_t o = words; words += (w + 63) & ~size_t(63); return o; };
+    size_t o_rng = take(Pz), o_smp = take(Pz), o_depth = take(Pz), o_col = take(3 * Pz),
+           o_light = take(kMaxDepth * Pz), o_ray = take(6 * Pz), o_hit = take(3 * Pz),
+           o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(Pz), o_q1 = take(Pz),
+           o_qs = take(Pz), o_ctl = take(kCtlWords), o_tot = take(16), o_ovf = take(ovf_words);
+    if (ensure_ws(s, words * 4)) return -1;
+    uint32_t* w = (uint32_t*)s.ws;
+    WfState st;
+    st.rng = w + o_rng;
+    st.smp = w + o_smp;
+    st.depth = w + o_depth;
+    st.col = (float*)(w + o_col);
+    st.light = (float*)(w + o_light);
+    st.ray = (float*)(w + o_ray);
+    st.hit = (float*)(w + o_hit);
+    st.hid = (int32_t*)(w + o_hid);
+    st.sho = (float*)(w + o_sho);
+    st.q[0] = w + o_q0;
+    st.q[1] = w + o_q1;
+    st.qs = w + o_qs;
+    st.ctl = w + o_ctl;
+    st.tot = (unsigned long long*)(w + o_tot);
+    st.P = P;
+    uint32_t* ovf = w + o_ovf;
+    hipStream_t str = s.stream;
+
+    TMPT_HIP(hipMemsetAsync(st.ctl, 0, kCtlWords * 4, str));
+    TMPT_HIP(hipMemsetAsync(st.tot, 0, 8 * sizeof(unsigned long long), str));
+    uint32_t p32 = (uint32_t)P;
+    TMPT_HIP(hipMemcpyAsync(st.ctl + kCtlCount0, &p32, 4, hipMemcpyHostToDevice, str));
+    k_wf_generate<kBlk><<<(int)((P + kBlk - 1) / kBlk), kBlk, 0, str>>>(a, st);
+
+    // per-launch timing of the traversal kernels
+    std::vector<hipEvent_t> ev;
+    auto new_ev = [&]() {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        ev.push_back(e);
+        return e;
+    };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ext_ev, sh_ev;
+    uint32_t* h_cnt = nullptr;
+    TMPT_HIP(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
+    const int kCheck = 8;
+    int parity = 0;
+    int64_t it = 0;
+    int rc = 0;
+    for (;;) {
+        for (int k = 0; k < kCheck; ++k, ++it) {
+            hipEvent_t e0 = new_ev(), e1 = new_ev(), e2 = new_ev(), e3 = new_ev();
+            (void)hipEventRecord(e0, str);
+            trace_e<<<grid_t, kBlk, 0, str>>>(view(s), st, parity, ovf);
+            (void)hipEventRecord(e1, str);
+            k_wf_shade<kBlk><<<grid_sh, kBlk, 0, str>>>(view(s), a, st, parity, d_out);
+            (void)hipEventRecord(e2, str);
+            trace_s<<<grid_t, kBlk, 0, str>>>(view(s), st, parity, ovf);
+            (void)hipEventRecord(e3, str);
+            k_wf_advance<<<1, 1, 0, str>>>(st, parity);
+            ext_ev.push_back({e0, e1});
+            sh_ev.push_back({e2, e3});
+            parity ^= 1;
+        }
+        if (hipGetLastError() != hipSuccess) { rc = -1; break; }
+        if (hipMemcpyAsync(h_cnt, st.ctl, 8, hipMemcpyDeviceToHost, str) != hipSuccess ||
+            hipStreamSynchronize(str) != hipSuccess) { rc = -1; break; }
+        if (h_cnt[0] == 0 && h_cnt[1] == 0) break;
+        if (it > (int64_t)a.spp * (kMaxDepth + 2) + 64) {  // cannot happen: each pixel needs <= spp*(kMaxDepth+1) iterations
+            set_error("wavefront: iteration bound exceeded");
+            rc = -3;
+            break;
+        }
+    }
+    unsigned long long tot[6] = {0, 0, 0, 0, 0, 0};
+    if (rc == 0) {
+        TMPT_HIP(hipMemcpyAsync(tot, st.tot, sizeof(tot), hipMemcpyDeviceToHost, str));
+        TMPT_HIP(hipStreamSynchronize(str));
+    }
+    double ems = 0, sms = 0;
+    for (auto& pr : ext_ev) { float ms = 0; (void)hipEventElapsedTime(&ms, pr.first, pr.second); ems += ms; }
+    for (auto& pr : sh_ev) { float ms = 0; (void)hipEventElapsedTime(&ms, pr.first, pr.second); sms += ms; }
+    for (auto e : ev) (void)hipEventDestroy(e);
+    (void)hipHostFree(h_cnt);
+    if (rc) {
+        if (rc == -1) set_error("wavefront: HIP error");
+        return rc;
+    }
+    s.extend_ms = ems;
+    s.shadow_ms = sms;
+    s.extend_rays = tot[0];
+    s.shadow_rays = tot[1];
+    s.node_visits = tot[2];
+    s.tri_tests = tot[3];
+    s.shadow_node_visits = tot[4];
+    s.shadow_tri_tests = tot[5];
+    s.extend_launches = it;
+    s.shadow_launches = it;
+    s.iterations = it;
+    return 0;
+}
+
+int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
+                    float* d_hits, int32_t* d_ids)
+{
+    auto fn = any ? k_intersect<true, kBlk, kSL> : k_intersect<false, kBlk, kSL>;
+    int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (n + kBlk - 1) / kBlk));
+    size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);
+    if (ensure_ws(s, ovf_bytes)) return -1;
+    fn<<<grid, kBlk, 0, s.stream>>>(view(s), d_rays, n, tmin, tmax, d_hits, d_ids, (uint32_t*)s.ws);
+    TMPT_HIP(hipGetLastError());
+    return 0;
+}
+
+int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t* d_out,
+           uint64_t* ray_count)
+{
+    RenderArgs a = make_args(cam, d);
+    bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
+    unsigned long long* d_counters = nullptr;
+    TMPT_HIP(hipMallocAsync((void**)&d_counters, 4 * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipMemsetAsync(d_counters, 0, 4 * sizeof(unsigned long long), s.stream));
+    hipEvent_t e0, e1;
+    TMPT_HIP(hipEventCreate(&e0));
+    TMPT_HIP(hipEventCreate(&e1));
+    TMPT_HIP(hipEventRecord(e0, s.stream));
+    int rc = 0;
+    bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode == TMPT_SEED_PIXEL;
+    s.extend_ms = s.shadow_ms = 0;
+    s.extend_rays = s.shadow_rays = s.node_visits = s.tri_tests = 0;
+    s.shadow_node_visits = s.shadow_tri_tests = 0;
+    s.extend_launches = s.shadow_launches = s.iterations = 0;
+    if (a.slots > 0) {
+        if (wave) rc = render_wavefront(s, a, d_out, count);
+        else rc = render_megakernel(s, a, d_out, count, d_counters);
+    }
+    (void)hipEventRecord(e1, s.stream);
+    hipError_t se = hipStreamSynchronize(s.stream);
+    unsigned long long c[4] = {0, 0, 0, 0};
+    if (rc == 0 && se == hipSuccess)
+        se = hipMemcpy(c, d_counters, sizeof(c), hipMemcpyDeviceToHost);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFreeAsync(d_counters, s.stream);
+    if (rc) return rc;
+    if (se != hipSuccess) {
+        set_error(std::string("render: ") + hipGetErrorString(se));
+        return -1;
+    }
+    s.render_ms = ms;
+    if (!wave) {
+        s.extend_ms = ms;
+        s.extend_rays = c[0];
+        s.node_visits = c[1];
+        s.tri_tests = c[2];
+        s.extend_launches = 1;
+    }
+    if (ray_count) *ray_count = wave ? (s.extend_rays + s.shadow_rays) : c[0];
+    return 0;
+}
+
+}  // namespace tmpt
