@@ -38,6 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "data"))
 import numpy as np  # noqa: E402
 
 import toymeshpathtracer_amd as tm  # noqa: E402  (imports torch first: one HIP runtime)
+from toymeshpathtracer_amd import shard as sharding  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -101,13 +102,12 @@ def main() -> None:
     init_s = time.perf_counter() - t0
     st0 = scene.stats()
 
-    rows_of = [tm.tile_row_to_y(W, H, BAND_ROWS, s, world) for s in range(world)]
+    rows_of = sharding.all_rows(H, BAND_ROWS, world)
     max_rows = max(len(r) for r in rows_of)
     my_rows = len(rows_of[rank])
     tile = torch.zeros((max_rows, W, 4), dtype=torch.uint8, device=dev)
     gathered = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
     image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
-    row_index = [torch.as_tensor(r, device=dev) for r in rows_of] if rank == 0 else None
 
     def step():
         _, rays = scene.trace_image(cam, W, H, SPP, seed_mode=tm.SEED_PIXEL, engine=engine,
@@ -117,9 +117,7 @@ def main() -> None:
         if world > 1:
             dist.gather(tile, gathered, dst=0)
         if rank == 0:  # de-interleave the bands into the frame, on the device
-            parts = gathered if world > 1 else [tile]
-            for s in range(world):
-                image.index_copy_(0, row_index[s], parts[s][: len(rows_of[s])])
+            sharding.assemble(gathered if world > 1 else [tile], rows_of, image)
         return rays, st
 
     for _ in range(args.warmup):

@@ -152,6 +152,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     (void)hipSetDevice(s.device);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.nodes) (void)hipFree(s.nodes);
+    if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);

@@ -19,6 +19,8 @@
 // :319) and of bench.py; it is timed separately (Scene::build_ms).
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -223,6 +225,7 @@ __device__ __forceinline__ int delta(const uint32_t* __restrict__ keys, int32_t 
 // Trees" (HPG 2012), Fig. 4.  Children: >=0 internal, <0 leaf (~slot).
 __global__ void __launch_bounds__(kBlock) k_karras(const uint32_t* __restrict__ keys, int32_t n,
                                                    int2* __restrict__ child,
+                                                   int2* __restrict__ range,
                                                    int32_t* __restrict__ parent_int,
                                                    int32_t* __restrict__ parent_leaf)
 {
@@ -247,6 +250,7 @@ __global__ void __launch_bounds__(kBlock) k_karras(const uint32_t* __restrict__ 
     int c0 = (lo == gamma) ? ~gamma : gamma;
     int c1 = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
     child[i] = make_int2(c0, c1);
+    range[i] = make_int2(lo, hi);  // the node covers sorted leaf slots lo..hi
     if (c0 < 0) parent_leaf[~c0] = i; else parent_int[c0] = i;
     if (c1 < 0) parent_leaf[~c1] = i; else parent_int[c1] = i;
     if (i == 0) parent_int[0] = -1;
@@ -309,6 +313,114 @@ __global__ void __launch_bounds__(kBlock) k_assemble(const int2* __restrict__ ch
     nodes[i].d = make_int4(c.x, c.y, depth[i], 0);
 }
 
+// ---------------------------------------------------------------- BVH4Q collapse
+__device__ __forceinline__ void node_or_leaf_box(int c, const Soa6& leaf,
+                                                 const uint32_t* __restrict__ vals, const Soa6& ib,
+                                                 float b[6])
+{
+    child_box(c, leaf, vals, ib, b);
+}
+
+__device__ __forceinline__ float box_area(const float b[6])
+{
+    float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+// One level of the top-down BVH2 -> BVH4Q collapse.  Each frontier entry
+// (BVH2 node, BVH4 slot) takes up to 4 children by repeatedly opening the
+// largest-area internal child; a BVH2 subtree of <= leaf_max triangles becomes
+// one leaf over its contiguous range of sorted slots (LBVH subtrees are
+// contiguous).  Child boxes are quantised outward to 8 bits in the node frame.
+__global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ child,
+                                                       const int2* __restrict__ range, Soa6 leaf,
+                                                       const uint32_t* __restrict__ vals, Soa6 ib,
+                                                       const int2* __restrict__ frontier, int nf,
+                                                       int2* __restrict__ next,
+                                                       uint32_t* __restrict__ counters,
+                                                       Bvh4Node* __restrict__ out, int leaf_max)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nf) return;
+    const int src = frontier[i].x, dst = frontier[i].y;
+    int cand[4];
+    int nc;
+    auto count_of = [&](int c) { return c < 0 ? 1 : range[c].y - range[c].x + 1; };
+    if (src < 0 || count_of(src) <= leaf_max) {  // whole (small) tree is one leaf
+        cand[0] = src;
+        nc = 1;
+    } else {
+        cand[0] = child[src].x;
+        cand[1] = child[src].y;
+        nc = 2;
+        while (nc < 4) {
+            int best = -1;
+            float best_a = -1.0f;
+            for (int k = 0; k < nc; ++k) {
+                int c = cand[k];
+                if (c >= 0 && count_of(c) > leaf_max) {
+                    float b[6];
+                    node_or_leaf_box(c, leaf, vals, ib, b);
+                    float a = box_area(b);
+                    if (a > best_a) { best_a = a; best = k; }
+                }
+            }
+            if (best < 0) break;
+            int c = cand[best];
+            cand[best] = child[c].x;
+            cand[nc++] = child[c].y;
+        }
+    }
+    float bx[4][6];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < nc; ++k) {
+        node_or_leaf_box(cand[k], leaf, vals, ib, bx[k]);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], bx[k][a]);
+            hi[a] = fmaxf(hi[a], bx[k][3 + a]);
+        }
+    }
+    uint32_t ebits = 0, mask = 0;
+    uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+    double scale[3];
+    for (int a = 0; a < 3; ++a) {
+        double ext = (double)hi[a] - (double)lo[a];
+        int e = (int)ceil(log2(fmax(ext, 1e-30) / 255.0));
+        e = max(-126, min(127, e));
+        scale[a] = ldexp(1.0, e);
+        ebits |= (uint32_t)(e + 127) << (8 * a);
+    }
+    int4 links = make_int4(0, 0, 0, 0);
+    int* lk = &links.x;
+    for (int k = 0; k < nc; ++k) {
+        for (int a = 0; a < 3; ++a) {
+            double l = floor(((double)bx[k][a] - (double)lo[a]) / scale[a]);
+            double h = ceil(((double)bx[k][3 + a] - (double)lo[a]) / scale[a]);
+            uint32_t ql = (uint32_t)fmin(fmax(l, 0.0), 255.0);
+            uint32_t qh = (uint32_t)fmin(fmax(h, 0.0), 255.0);
+            qlo[a] |= ql << (8 * k);
+            qhi[a] |= qh << (8 * k);
+        }
+        mask |= 1u << k;
+        int c = cand[k];
+        if (c < 0) {  // BVH2 leaf: one triangle at sorted slot ~c
+            lk[k] = (int)(0x80000000u | (uint32_t)(~c));
+        } else if (count_of(c) <= leaf_max) {
+            lk[k] = (int)(0x80000000u | ((uint32_t)(count_of(c) - 1) << kLeafCountShift) |
+                          (uint32_t)range[c].x);
+        } else {
+            uint32_t slot = atomicAdd(&counters[0], 1u);
+            uint32_t qi = atomicAdd(&counters[1], 1u);
+            next[qi] = make_int2(c, (int)slot);
+            lk[k] = (int)slot;
+        }
+    }
+    out[dst].a = f4(lo[0], lo[1], lo[2], __uint_as_float(ebits | (mask << 24)));
+    out[dst].b = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
+    out[dst].c = make_uint4(qlo[2], qhi[2], 0u, 0u);
+    out[dst].d = links;
+}
+
 __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tris9, int32_t n,
                                                     const uint32_t* __restrict__ vals,
                                                     TriPre* __restrict__ pre)
@@ -345,6 +457,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
     const int32_t m = n >= 2 ? n - 1 : 1;  // internal nodes
     s.n_nodes = m;
     TMPT_HIP(hipMalloc(&s.nodes, sizeof(BvhNode) * (size_t)m));
+    TMPT_HIP(hipMalloc(&s.nodes4, sizeof(Bvh4Node) * (size_t)m));
     TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * (size_t)std::max(n, 1)));
     TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(n, 1)));
     if (n == 0) {
@@ -376,12 +489,16 @@ int build_lbvh(Scene& s, const float* d_tris9)
     uint32_t* v1 = (uint32_t*)alloc(nn * 4);
     uint32_t* hist = (uint32_t*)alloc((size_t)256 * nb_sort * 4);
     int2* child = (int2*)alloc((size_t)m * sizeof(int2));
+    int2* range = (int2*)alloc((size_t)m * sizeof(int2));
+    int2* fr0 = (int2*)alloc((size_t)m * sizeof(int2));
+    int2* fr1 = (int2*)alloc((size_t)m * sizeof(int2));
+    uint32_t* c4 = (uint32_t*)alloc(2 * sizeof(uint32_t));
     int32_t* pint = (int32_t*)alloc((size_t)m * 4);
     int32_t* pleaf = (int32_t*)alloc(nn * 4);
     int32_t* depth = (int32_t*)alloc((size_t)m * 4);
     int32_t* maxd = (int32_t*)alloc(4);
     if (!leafbuf || !ibbuf || !cent || !cb || !k0 || !v0 || !k1 || !v1 || !hist || !child ||
-        !pint || !pleaf || !depth || !maxd) {
+        !range || !fr0 || !fr1 || !c4 || !pint || !pleaf || !depth || !maxd) {
         free_all();
         set_error("build_lbvh: out of device memory");
         return -1;
@@ -410,9 +527,8 @@ int build_lbvh(Scene& s, const float* d_tris9)
         if (n == 1) {
             k_single<<<1, 1, 0, st>>>(leaf, s.nodes);
             s.max_depth = 0;
-            break;
-        }
-        k_karras<<<blocks_for(m, kBlock), kBlock, 0, st>>>(ki, n, child, pint, pleaf);
+        } else {
+            k_karras<<<blocks_for(m, kBlock), kBlock, 0, st>>>(ki, n, child, range, pint, pleaf);
         k_depth<<<blocks_for(m, kBlock), kBlock, 0, st>>>(pint, m, depth, maxd);
         int32_t hmax = 0;
         if (hipMemcpyAsync(&hmax, maxd, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -423,9 +539,39 @@ int build_lbvh(Scene& s, const float* d_tris9)
             rc = -2;
             break;
         }
-        for (int L = hmax; L >= 0; --L)
-            k_refit_level<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, L, leaf, vi, ib);
-        k_assemble<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, leaf, vi, ib, s.nodes);
+            for (int L = hmax; L >= 0; --L)
+                k_refit_level<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, L, leaf, vi, ib);
+            k_assemble<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, leaf, vi, ib, s.nodes);
+        }
+        // BVH2 -> BVH4Q, top-down, one launch per level
+        int leaf_max = 2;
+        if (const char* e = getenv("TMPT_LEAF_MAX")) leaf_max = std::max(1, std::min(kLeafMaxTris, atoi(e)));
+        s.leaf_max = leaf_max;
+        int2 root = make_int2(n == 1 ? ~0 : 0, 0);
+        uint32_t hc[2] = {1u, 0u};
+        if (hipMemcpyAsync(fr0, &root, sizeof(root), hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(c4, hc, sizeof(hc), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
+        int nf = 1, levels = 0;
+        int2 *fa = fr0, *fb = fr1;
+        while (nf > 0) {
+            k_bvh4_level<<<blocks_for(nf, kBlock), kBlock, 0, st>>>(child, range, leaf, vi, ib, fa, nf, fb,
+                                                                    c4, s.nodes4, leaf_max);
+            ++levels;
+            if (hipMemcpyAsync(hc, c4, sizeof(hc), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }
+            nf = (int)hc[1];
+            hc[1] = 0;
+            if (hipMemcpyAsync(c4 + 1, &hc[1], 4, hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
+            std::swap(fa, fb);
+        }
+        if (rc) break;
+        s.n_nodes4 = (int32_t)hc[0];
+        s.depth4 = levels;
+        if (3 * levels + 1 > kStackTotal) {
+            set_error("build_lbvh: BVH4 depth " + std::to_string(levels) + " exceeds the traversal stack");
+            rc = -2;
+            break;
+        }
     } while (0);
     hipError_t e = hipGetLastError();
     hipError_t e2 = hipStreamSynchronize(st);

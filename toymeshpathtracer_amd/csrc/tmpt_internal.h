@@ -29,6 +29,26 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node is one half cache line");
 
+// 4-wide node with quantised child boxes (DESIGN.md "BVH4Q"): 64 B, one
+// half cache line, 4 x dwordx4 loads for FOUR child boxes.
+//   a: origin.xyz (node box min, f32), w = exponents ex,ey,ez (bytes 0-2,
+//      biased by 127: scale = 2^(e-127)) | child-valid mask (byte 3)
+//   b: qlo.x[4], qhi.x[4], qlo.y[4], qhi.y[4]   (uint8 per child, child k in byte k)
+//   c: qlo.z[4], qhi.z[4], 0, 0
+//   d: child links: >=0 node index; <0 leaf = 0x80000000 | (count-1)<<27 | first slot
+// A child box decodes as origin + q*scale (q*scale exact), quantised outward
+// from the padded boxes, so culling stays conservative.
+struct alignas(16) Bvh4Node {
+    float4 a;
+    uint4 b;
+    uint4 c;
+    int4 d;
+};
+static_assert(sizeof(Bvh4Node) == 64, "BVH4Q node is one half cache line");
+constexpr int kLeafCountShift = 27;
+constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
+constexpr int kLeafMaxTris = 16;
+
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x
     float4 b;  // e1.yz, e2.xy
@@ -47,10 +67,11 @@ struct alignas(16) TriOrig {
 constexpr float kBoxPadRel = 1e-5f;
 constexpr float kTfarSlack = 1.00001f;
 
-// Stack: kStackLds entries per lane live in LDS, the rest spill to a global
-// per-lane area.  An LBVH over (30-bit Morton, index) keys has depth <= 62, so
-// kStackTotal = 64 always suffices (DESIGN.md "Traversal").
-constexpr int kStackTotal = 64;
+// Stack: SL entries per lane live in LDS, the rest spill to a global per-lane
+// area.  BVH2: depth <= 62 for (30-bit Morton, index) keys, <= depth+1 entries;
+// BVH4Q: <= 3 per level.  The build rejects trees that could exceed
+// kStackTotal (DESIGN.md "Traversal").
+constexpr int kStackTotal = 128;
 
 struct Scene {
     int device = 0;
@@ -58,6 +79,8 @@ struct Scene {
     int32_t n_nodes = 0;    // internal nodes
     int32_t max_depth = 0;  // of the LBVH
     BvhNode* nodes = nullptr;
+    Bvh4Node* nodes4 = nullptr;
+    int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0;
     TriPre* tri_pre = nullptr;
     TriOrig* tri_orig = nullptr;
     const float2* sincos = nullptr;  // borrowed from the per-device table

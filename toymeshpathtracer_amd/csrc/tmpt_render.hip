@@ -14,6 +14,9 @@
 //    unmodified reference RNG chain, H-way parallel -- a correctness mode).
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
 #include <chrono>
 #include <vector>
@@ -78,7 +81,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long* counters, uint3
 }
 
 // ============================================================ megakernel
-template <bool COUNT, int BLOCK, int SL>
+template <bool WIDE, bool COUNT, int BLOCK, int SL>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
                                          TravCount& cnt)
@@ -88,13 +91,13 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
         ++rays;
         float t, u, v;
-        int id = traverse<false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+        int id = traverse<WIDE, false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
             ++rays;  // shadow ray, main.cpp:57-59
             float ts, us, vs;
-            int sid = traverse<true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT, ts,
+            int sid = traverse<WIDE, true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT, ts,
                                             us, vs, st, cnt);
             lbuf[depth * BLOCK] = sid >= 0 ? 0.0f : light_cosine(nrm, d);
             f3 rnd = random_unit_vector(rng, sv.sincos);  // main.cpp:71-72
@@ -111,7 +114,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     return color;
 }
 
-template <bool COUNT, int BLOCK, int SL>
+template <bool WIDE, bool COUNT, int BLOCK, int SL>
 __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const RenderArgs& a, int x,
                                                  int y, uint32_t& rng, uint32_t& rays,
                                                  TravStack<BLOCK, SL>& st, float* lbuf,
@@ -121,12 +124,12 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
     for (int s = 0; s < a.spp; ++s) {  // main.cpp:209-219
         f3 o, d;
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-        col = col + trace_path<COUNT>(sv, o, d, rng, rays, st, lbuf, cnt);
+        col = col + trace_path<WIDE, COUNT>(sv, o, d, rng, rays, st, lbuf, cnt);
     }
     return pack_pixel(col, a.spp_recip);
 }
 
-template <bool ROW, bool COUNT, int BLOCK, int SL>
+template <bool WIDE, bool ROW, bool COUNT, int BLOCK, int SL>
 __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -147,19 +150,19 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
             int y = tile_row_to_y(a, lr);
             uint32_t rng = row_seed((uint32_t)y);  // main.cpp:204, unmodified
             for (int x = 0; x < a.W; ++x)
-                out[(int64_t)lr * a.W + x] = render_pixel<COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+                out[(int64_t)lr * a.W + x] = render_pixel<WIDE, COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
         } else {
             int lr = (int)(w / a.W), x = (int)(w - (int64_t)lr * a.W);
             int y = tile_row_to_y(a, lr);
             uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)a.W);
-            out[w] = render_pixel<COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+            out[w] = render_pixel<WIDE, COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
         }
     }
     flush_counts<BLOCK, COUNT>(counters, rays, cnt);
 }
 
 // ============================================================ batched HitScene
-template <bool ANY, int BLOCK, int SL>
+template <bool WIDE, bool ANY, int BLOCK, int SL>
 __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* __restrict__ rays,
                                                      int64_t n, float tmin, float tmax,
                                                      float* __restrict__ hits,
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         const float* r = rays + 6 * i;
         f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
         float t, u, v;
-        int id = traverse<ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
+        int id = traverse<WIDE, ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
         ids[i] = id;
         if (id >= 0) {
             f3 pos, nrm;
@@ -188,6 +191,19 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
 }
 
 // ============================================================ wavefront
+// Queues are segmented: the P path slots are cut into kSeg contiguous ranges
+// of seg_cap slots (seg_cap a multiple of the 256-slot shade block); segment j
+// of a queue holds only entries of slots in range j, at [j*seg_cap, +count_j).
+// Every counter and fetch head sits on its own 64-B line, so the producers'
+// wave appends and the consumers' chunk reservations spread over kSeg words
+// instead of serialising on one (MI355X_MICROARCH.md: one word saturates at
+// ~88 atomics/us).
+constexpr int kSeg = 64;
+constexpr int kCtr = 16;  // words between counters (64 B)
+constexpr uint32_t kChunk = 64;  // queue entries a wave reserves per atomic
+constexpr uint32_t kSkip = 0x80000000u;  // queue-entry flag: path stopped at kMaxDepth
+constexpr uint32_t kDone = 0xFFFFFFFFu;  // depth value of a finished pixel
+
 struct WfState {
     uint32_t* rng;
     uint32_t* smp;
@@ -198,19 +214,27 @@ struct WfState {
     float* hit;    // [3][P]  t u v
     int32_t* hid;  // [P]
     float* sho;    // [3][P] shadow origin
-    uint32_t* q[2];
-    uint32_t* qs;
-    uint32_t* ctl;  // control words, see kCtl*
+    uint32_t* q[2];  // extend queues (per parity), kSeg * seg_cap entries
+    uint32_t* qs;    // shadow queue
+    uint32_t* cnt[2];  // extend queue counts per parity, kSeg counters (stride kCtr)
+    uint32_t* cnt_s;   // shadow queue counts
+    uint32_t* head_e;  // fetch heads
+    uint32_t* head_s;
+    uint32_t* total;   // [0]: entries of the queue the next iteration consumes
     unsigned long long* tot;  // [0] extend rays [1] shadow rays [2,3] extend node/tri visits [4,5] shadow
     int64_t P;
+    uint32_t seg_cap;
 };
-// control words (uint32): queue counts per parity, shadow count, fetch heads
-enum { kCtlCount0 = 0, kCtlCount1 = 1, kCtlShadow = 2, kCtlHeadE = 3, kCtlHeadS = 4, kCtlWords = 16 };
 
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 {
     int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (p < kSeg) {  // initial queue: every slot, in slot order
+        int64_t lo = p * s.seg_cap;
+        int64_t c = s.P - lo;
+        s.cnt[0][p * kCtr] = (uint32_t)(c < 0 ? 0 : (c > s.seg_cap ? s.seg_cap : c));
+    }
     if (p >= s.P) return;
     int lr = (int)(p / a.W), x = (int)(p - (int64_t)lr * a.W);
     int y = tile_row_to_y(a, lr);
@@ -224,12 +248,19 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
     s.col[p] = 0.0f; s.col[P + p] = 0.0f; s.col[2 * P + p] = 0.0f;
     s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
     s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
-    s.q[0][p] = (uint32_t)p;
+    s.q[0][p] = (uint32_t)p;  // segment j starts at j*seg_cap = its first slot
 }
 
-// Persistent traversal over a queue: each wave takes 64 queue entries at a
-// time from a fetch head (one atomic per wave) until the queue is drained.
-template <bool ANY, bool COUNT, int BLOCK, int SL>
+// Persistent traversal with lane refill ("dynamic fetch", Aila & Laine 2009,
+// re-derived for wave64 and segmented queues): every lane keeps a resumable
+// traversal state in registers.  A wave holds a reservation of up to kChunk
+// queue entries (uniform, in SGPRs); whenever >= REFILL lanes are idle they
+// take the next entries of the reservation (ballot + mbcnt ranks).  An empty
+// reservation is renewed by ONE atomic on the head of the wave's current
+// segment; exhausted segments are skipped, starting from the wave's own, so
+// waves work on nearby pixels and the heads see few atomics.  Lanes run
+// STEPS traversal steps between refill checks.
+template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 16>
 __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int parity,
                                                     uint32_t* __restrict__ ovf)
 {
@@ -239,41 +270,88 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
     TravCount cnt;
     uint32_t traced = 0;
     const uint32_t* q = ANY ? s.qs : s.q[parity];
-    const uint32_t n = ANY ? s.ctl[kCtlShadow] : s.ctl[kCtlCount0 + parity];
-    uint32_t* head = &s.ctl[ANY ? kCtlHeadS : kCtlHeadE];
+    const uint32_t* counts = ANY ? s.cnt_s : s.cnt[parity];
+    uint32_t* heads = ANY ? s.head_s : s.head_e;
     const int64_t P = s.P;
     const f3 ldir = light_dir();
+    const uint64_t lt = (1ull << lane_id()) - 1ull;
+    const uint32_t wave_gid = (uint32_t)(gtid >> 6);
+    uint32_t seg = wave_gid % kSeg, seg_left = kSeg;  // segments not yet found exhausted
+    uint32_t res = 0, res_end = 0;                    // reservation [res, res_end) of queue positions
+    bool active = false;
+    uint32_t p = 0;
+    TravRay r;
+    TravState ts;
     for (;;) {
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(head, 64u);
-        base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        uint32_t i = base + (uint32_t)lane_id();
-        if (i < n) {
-            uint32_t p = q[i];
-            if (ANY) {
-                f3 o = mk(s.sho[p], s.sho[P + p], s.sho[2 * P + p]);
-                float t, u, v;
-                int id = traverse<true, COUNT>(sv, make_trav_ray(o, ldir), kMinT, kMaxT, t, u, v, st, cnt);
-                ++traced;
-                if (id >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
-            } else if (s.depth[p] < (uint32_t)kMaxDepth) {
-                f3 o = mk(s.ray[p], s.ray[P + p], s.ray[2 * P + p]);
-                f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
-                float t, u = 0.0f, v = 0.0f;
-                int id = traverse<false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
-                ++traced;
-                s.hid[p] = id;
-                s.hit[P + p] = u;
-                s.hit[2 * P + p] = v;
+        uint64_t idle = __ballot(!active);
+        uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nidle >= (uint32_t)REFILL && (res < res_end || seg_left > 0)) {
+            while (res >= res_end && seg_left > 0) {  // renew the reservation (wave-uniform)
+                uint32_t c = counts[seg * kCtr];
+                uint32_t h = __hip_atomic_load(&heads[seg * kCtr], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t b = c;
+                if (h < c) {
+                    if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
+                    b = (uint32_t)__shfl((int)b, 0);
+                }
+                if (b < c) {
+                    res = seg * s.seg_cap + b;
+                    res_end = seg * s.seg_cap + min(b + kChunk, c);
+                } else {
+                    seg = seg + 1 == kSeg ? 0 : seg + 1;
+                    --seg_left;
+                }
+            }
+            uint32_t take = min(nidle, res_end - res);
+            uint32_t k = (uint32_t)__popcll(idle & lt);
+            if (!active && k < take) {
+                uint32_t e = q[res + k];
+                if (!(e & kSkip)) {  // flagged entries: stopped at kMaxDepth, nothing to trace
+                    p = e;
+                    f3 o, d;
+                    if (ANY) {
+                        o = mk(s.sho[p], s.sho[P + p], s.sho[2 * P + p]);
+                        d = ldir;
+                    } else {
+                        o = mk(s.ray[p], s.ray[P + p], s.ray[2 * P + p]);
+                        d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
+                    }
+                    r = make_trav_ray(o, d);
+                    trav_init(ts, kMaxT);
+                    active = true;
+                    ++traced;
+                }
+            }
+            res += take;
+        }
+        if (!__any(active)) {
+            if (res >= res_end && seg_left == 0) break;
+            continue;
+        }
+        if (active) {
+            bool done = false;
+            for (int k = 0; k < STEPS; ++k) {
+                done = trav_step_w<WIDE, ANY, COUNT>(sv, r, 0.0f, kMinT, kMaxT, ts, st, cnt);
+                if (done) break;
+            }
+            if (done) {
+                active = false;
+                if (ANY) {
+                    if (ts.best >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
+                } else {
+                    s.hid[p] = ts.best;
+                    s.hit[P + p] = ts.bu;
+                    s.hit[2 * P + p] = ts.bv;
+                }
             }
         }
     }
-    uint32_t r = wave_sum(traced);
+    uint32_t rr = wave_sum(traced);
     uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
     uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
     if (lane_id() == 0) {
-        atomicAdd(&s.tot[ANY ? 1 : 0], (unsigned long long)r);
+        atomicAdd(&s.tot[ANY ? 1 : 0], (unsigned long long)rr);
         if (COUNT) {
             atomicAdd(&s.tot[ANY ? 4 : 2], (unsigned long long)nv);
             atomicAdd(&s.tot[ANY ? 5 : 3], (unsigned long long)nt);
@@ -281,93 +359,96 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
     }
 }
 
-// shade: consumes the extend queue of `parity`, appends to the other parity's
-// queue and to the shadow queue; writes finished pixels.
+// shade: one lane per path slot, in slot order, so every state access is
+// coalesced.  Every unfinished path was extended this iteration (or stopped at
+// kMaxDepth), so each needs exactly one shading step.  Appends (wave-compacted)
+// to the block's segment of the other parity's extend queue and of the shadow
+// queue; writes finished pixels.
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, WfState s,
                                                     int parity, uint32_t* __restrict__ out)
 {
-    const uint32_t n = s.ctl[kCtlCount0 + parity];
-    uint32_t* qn = s.q[parity ^ 1];
     const int64_t P = s.P;
-    const int64_t stride = (int64_t)gridDim.x * BLOCK;
-    // all lanes iterate the same number of times (wave-uniform appends)
-    const int64_t iters = ((int64_t)n + stride - 1) / stride;
-    for (int64_t it = 0; it < iters; ++it) {
-        int64_t i = it * stride + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-        bool valid = i < (int64_t)n;
-        bool cont = false, shadow = false;
-        uint32_t p = valid ? s.q[parity][i] : 0u;
-        if (valid) {
-            uint32_t depth = s.depth[p];
-            uint32_t rng = s.rng[p];
-            f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
-            int id = depth < (uint32_t)kMaxDepth ? s.hid[p] : -1;
-            bool finish = true;
-            f3 color = mk(0.0f, 0.0f, 0.0f);
-            if (depth < (uint32_t)kMaxDepth) {
-                if (id >= 0) {  // Scatter, main.cpp:44-73
-                    f3 pos, nrm;
-                    hit_record(sv, id, s.hit[P + p], s.hit[2 * P + p], pos, nrm);
-                    s.light[(int64_t)depth * P + p] = light_cosine(nrm, d);  // zeroed by shadow if occluded
-                    s.sho[p] = pos.x; s.sho[P + p] = pos.y; s.sho[2 * P + p] = pos.z;
-                    f3 rnd = random_unit_vector(rng, sv.sincos);
-                    f3 target = pos + nrm + rnd;
-                    d = normalize(target - pos);
-                    s.ray[p] = pos.x; s.ray[P + p] = pos.y; s.ray[2 * P + p] = pos.z;
-                    s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
-                    ++depth;
-                    shadow = true;
-                    cont = true;  // depth == kMaxDepth: finished next iteration, after its shadow
-                    finish = false;
-                } else {
-                    color = sky(d);  // main.cpp:106-107
-                }
+    const int64_t p64 = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t p = (uint32_t)p64;
+    const uint32_t seg = (uint32_t)(((int64_t)blockIdx.x * BLOCK) / s.seg_cap);
+    uint32_t depth = p64 < P ? s.depth[p] : kDone;
+    bool cont = false, shadow = false;
+    if (depth != kDone) {
+        uint32_t rng = s.rng[p];
+        f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
+        int id = depth < (uint32_t)kMaxDepth ? s.hid[p] : -1;
+        bool finish = true;
+        f3 color = mk(0.0f, 0.0f, 0.0f);
+        if (depth < (uint32_t)kMaxDepth) {
+            if (id >= 0) {  // Scatter, main.cpp:44-73
+                f3 pos, nrm;
+                hit_record(sv, id, s.hit[P + p], s.hit[2 * P + p], pos, nrm);
+                s.light[(int64_t)depth * P + p] = light_cosine(nrm, d);  // zeroed by shadow if occluded
+                s.sho[p] = pos.x; s.sho[P + p] = pos.y; s.sho[2 * P + p] = pos.z;
+                f3 rnd = random_unit_vector(rng, sv.sincos);
+                f3 target = pos + nrm + rnd;
+                d = normalize(target - pos);
+                s.ray[p] = pos.x; s.ray[P + p] = pos.y; s.ray[2 * P + p] = pos.z;
+                s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
+                ++depth;
+                shadow = true;
+                cont = true;  // depth == kMaxDepth: finished next iteration, after its shadow
+                finish = false;
+            } else {
+                color = sky(d);  // main.cpp:106-107
             }
-            if (finish) {
-                for (int k = (int)depth - 1; k >= 0; --k)
-                    color = backward_step(color, s.light[(int64_t)k * P + p]);
-                f3 col = mk(s.col[p], s.col[P + p], s.col[2 * P + p]) + color;
-                uint32_t smp = s.smp[p] + 1;
-                s.smp[p] = smp;
-                depth = 0;
-                if (smp < (uint32_t)a.spp) {
-                    s.col[p] = col.x; s.col[P + p] = col.y; s.col[2 * P + p] = col.z;
-                    int lr = (int)(p / (uint32_t)a.W), x = (int)(p - (uint32_t)lr * (uint32_t)a.W);
-                    int y = tile_row_to_y(a, lr);
-                    f3 o;
-                    camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-                    s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
-                    s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
-                    cont = true;
-                } else {
-                    out[p] = pack_pixel(col, a.spp_recip);
-                }
-            }
-            s.depth[p] = depth;
-            s.rng[p] = rng;
         }
-        uint32_t qi = wave_append(&s.ctl[kCtlCount0 + (parity ^ 1)], cont);
-        if (cont) qn[qi] = p;
-        uint32_t si = wave_append(&s.ctl[kCtlShadow], shadow);
-        if (shadow) s.qs[si] = p;
+        if (finish) {
+            for (int k = (int)depth - 1; k >= 0; --k)
+                color = backward_step(color, s.light[(int64_t)k * P + p]);
+            f3 col = mk(s.col[p], s.col[P + p], s.col[2 * P + p]) + color;
+            uint32_t smp = s.smp[p] + 1;
+            s.smp[p] = smp;
+            depth = 0;
+            if (smp < (uint32_t)a.spp) {
+                s.col[p] = col.x; s.col[P + p] = col.y; s.col[2 * P + p] = col.z;
+                int lr = (int)(p / (uint32_t)a.W), x = (int)(p - (uint32_t)lr * (uint32_t)a.W);
+                int y = tile_row_to_y(a, lr);
+                f3 o;
+                camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
+                s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
+                s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
+                cont = true;
+            } else {
+                out[p] = pack_pixel(col, a.spp_recip);
+                depth = kDone;
+            }
+        }
+        s.depth[p] = depth;
+        s.rng[p] = rng;
     }
+    const uint32_t base = seg * s.seg_cap;
+    uint32_t qi = wave_append(&s.cnt[parity ^ 1][seg * kCtr], cont);
+    if (cont) s.q[parity ^ 1][base + qi] = depth == (uint32_t)kMaxDepth ? (p | kSkip) : p;
+    uint32_t si = wave_append(&s.cnt_s[seg * kCtr], shadow);
+    if (shadow) s.qs[base + si] = p;
 }
 
-// between iterations: retire the consumed queue, reset fetch heads
-__global__ void k_wf_advance(WfState s, int parity)
+// after the extend of `parity` was consumed: zero its counts and the heads;
+// publish the size of the next queue for the host's termination check
+__global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity)
 {
-    s.ctl[kCtlCount0 + parity] = 0;
-    s.ctl[kCtlHeadE] = 0;
-    s.ctl[kCtlHeadS] = 0;
-    s.ctl[kCtlShadow] = 0;
+    int j = threadIdx.x;
+    uint32_t next = s.cnt[parity ^ 1][j * kCtr];
+    s.cnt[parity][j * kCtr] = 0;
+    s.cnt_s[j * kCtr] = 0;
+    s.head_e[j * kCtr] = 0;
+    s.head_s[j * kCtr] = 0;
+    next = wave_sum(next);
+    if (j == 0) s.total[0] = next;
 }
 
 // ============================================================ host side
 namespace {
 
 constexpr int kBlk = 256;
-constexpr int kSL = 32;  // LDS stack entries per lane
+constexpr int kSL = 16;  // LDS stack entries per lane
 
 int occupancy_grid(const void* fn, int block, size_t dyn_lds, int device)
 {
@@ -394,7 +475,7 @@ int ensure_ws(Scene& s, size_t bytes)
 
 SceneView view(const Scene& s)
 {
-    return SceneView{s.nodes, s.tri_pre, s.tri_orig, s.sincos, s.n};
+    return SceneView{s.nodes, s.nodes4, s.tri_pre, s.tri_orig, s.sincos, s.n};
 }
 
 RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
@@ -423,10 +504,10 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     return a;
 }
 
-template <bool ROW, bool COUNT>
+template <bool WIDE, bool ROW, bool COUNT>
 int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long* counters)
 {
-    auto fn = k_mega<ROW, COUNT, kBlk, kSL>;
+    auto fn = k_mega<WIDE, ROW, COUNT, kBlk, kSL>;
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     int64_t items = ROW ? a.tile_rows : a.slots;
     grid = (int)std::min<int64_t>(grid, (items + kBlk - 1) / kBlk);
@@ -438,16 +519,28 @@ int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long
     return 0;
 }
 
+// BVH layout used by the traversal kernels: the 4-wide quantised BVH unless
+// TMPT_BVH=2 selects the plain LBVH2 (kept for A/B measurements).
+bool use_wide()
+{
+    const char* e = getenv("TMPT_BVH");
+    return !(e && atoi(e) == 2);
+}
+
 }  // namespace
 
 int render_megakernel(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
 {
-    bool row = a.seed_mode == TMPT_SEED_ROW;
-    if (row) return count ? launch_mega<true, true>(s, a, d_out, d_counters)
-                          : launch_mega<true, false>(s, a, d_out, d_counters);
-    return count ? launch_mega<false, true>(s, a, d_out, d_counters)
-                 : launch_mega<false, false>(s, a, d_out, d_counters);
+    const bool row = a.seed_mode == TMPT_SEED_ROW;
+    const bool wide = use_wide();
+#define TMPT_MEGA(W_, R_, C_) \
+    if (wide == W_ && row == R_ && count == C_) return launch_mega<W_, R_, C_>(s, a, d_out, d_counters);
+    TMPT_MEGA(true, true, true) TMPT_MEGA(true, true, false) TMPT_MEGA(true, false, true)
+    TMPT_MEGA(true, false, false) TMPT_MEGA(false, true, true) TMPT_MEGA(false, true, false)
+    TMPT_MEGA(false, false, true) TMPT_MEGA(false, false, false)
+#undef TMPT_MEGA
+    return -1;
 }
 
 // Wavefront driver.  The host enqueues iterations without reading the queue
@@ -456,21 +549,51 @@ int render_megakernel(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 {
     const int64_t P = a.slots;
-    const size_t Pz = (size_t)P;
-    auto trace_e = count ? k_wf_trace<false, true, kBlk, kSL> : k_wf_trace<false, false, kBlk, kSL>;
-    auto trace_s = count ? k_wf_trace<true, true, kBlk, kSL> : k_wf_trace<true, false, kBlk, kSL>;
+    if (P >= (int64_t)kSkip) {
+        set_error("wavefront: tile too large");
+        return -22;
+    }
+    const bool wide = use_wide();
+    auto trace_e = wide ? (count ? k_wf_trace<true, false, true, kBlk, kSL> : k_wf_trace<true, false, false, kBlk, kSL>)
+                        : (count ? k_wf_trace<false, false, true, kBlk, kSL> : k_wf_trace<false, false, false, kBlk, kSL>);
+    auto trace_s = wide ? (count ? k_wf_trace<true, true, true, kBlk, kSL> : k_wf_trace<true, true, false, kBlk, kSL>)
+                        : (count ? k_wf_trace<false, true, true, kBlk, kSL> : k_wf_trace<false, true, false, kBlk, kSL>);
+    int sl = kSL;
+    // TMPT_TUNE=<sl>,<steps>,<refill>: tuning variants of the traversal kernels
+    if (const char* tune = getenv("TMPT_TUNE")) {
+        int a0 = 0, a1 = 0, a2 = 0;
+        if (sscanf(tune, "%d,%d,%d", &a0, &a1, &a2) == 3 && !count) {
+#define TMPT_VARIANT(SL_, ST_, RF_)                                      \
+    if (wide && a0 == SL_ && a1 == ST_ && a2 == RF_) {                   \
+        trace_e = k_wf_trace<true, false, false, kBlk, SL_, ST_, RF_>;   \
+        trace_s = k_wf_trace<true, true, false, kBlk, SL_, ST_, RF_>;    \
+        sl = SL_;                                                        \
+    }
+            TMPT_VARIANT(16, 2, 16)
+            TMPT_VARIANT(16, 4, 16)
+            TMPT_VARIANT(16, 16, 16)
+            TMPT_VARIANT(32, 8, 16)
+            TMPT_VARIANT(16, 8, 8)
+            TMPT_VARIANT(16, 8, 32)
+            TMPT_VARIANT(24, 4, 16)
+#undef TMPT_VARIANT
+        }
+    }
     int grid_t = occupancy_grid((const void*)trace_e, kBlk, 0, s.device);
-    int grid_sh = 0, cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device);
-    grid_sh = cus * 8;
-    size_t ovf_words = (size_t)grid_t * kBlk * (kStackTotal - kSL);
+    const int grid_sh = (int)((P + kBlk - 1) / kBlk);
+    const size_t seg_cap = (size_t)(((P + kSeg - 1) / kSeg + kBlk - 1) / kBlk) * kBlk;
+    const size_t qcap = seg_cap * kSeg;
+    const size_t Pz = (size_t)P;
+    size_t ovf_words = (size_t)grid_t * kBlk * (kStackTotal - sl);
     // layout of the workspace
     size_t words = 0;
     auto take = [&](size_t w) { size_t o = words; words += (w + 63) & ~size_t(63); return o; };
+    const size_t ctr_words = (size_t)kSeg * kCtr;
     size_t o_rng = take(Pz), o_smp = take(Pz), o_depth = take(Pz), o_col = take(3 * Pz),
            o_light = take(kMaxDepth * Pz), o_ray = take(6 * Pz), o_hit = take(3 * Pz),
-           o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(Pz), o_q1 = take(Pz),
-           o_qs = take(Pz), o_ctl = take(kCtlWords), o_tot = take(16), o_ovf = take(ovf_words);
+           o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(qcap), o_q1 = take(qcap),
+           o_qs = take(qcap), o_ctl = take(5 * ctr_words + 64), o_tot = take(16),
+           o_ovf = take(ovf_words);
     if (ensure_ws(s, words * 4)) return -1;
     uint32_t* w = (uint32_t*)s.ws;
     WfState st;
@@ -486,17 +609,21 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     st.q[0] = w + o_q0;
     st.q[1] = w + o_q1;
     st.qs = w + o_qs;
-    st.ctl = w + o_ctl;
+    st.cnt[0] = w + o_ctl;
+    st.cnt[1] = st.cnt[0] + ctr_words;
+    st.cnt_s = st.cnt[1] + ctr_words;
+    st.head_e = st.cnt_s + ctr_words;
+    st.head_s = st.head_e + ctr_words;
+    st.total = st.head_s + ctr_words;
     st.tot = (unsigned long long*)(w + o_tot);
     st.P = P;
+    st.seg_cap = (uint32_t)seg_cap;
     uint32_t* ovf = w + o_ovf;
     hipStream_t str = s.stream;
 
-    TMPT_HIP(hipMemsetAsync(st.ctl, 0, kCtlWords * 4, str));
+    TMPT_HIP(hipMemsetAsync(w + o_ctl, 0, (5 * ctr_words + 64) * 4, str));
     TMPT_HIP(hipMemsetAsync(st.tot, 0, 8 * sizeof(unsigned long long), str));
-    uint32_t p32 = (uint32_t)P;
-    TMPT_HIP(hipMemcpyAsync(st.ctl + kCtlCount0, &p32, 4, hipMemcpyHostToDevice, str));
-    k_wf_generate<kBlk><<<(int)((P + kBlk - 1) / kBlk), kBlk, 0, str>>>(a, st);
+    k_wf_generate<kBlk><<<(int)((std::max<int64_t>(P, kSeg) + kBlk - 1) / kBlk), kBlk, 0, str>>>(a, st);
 
     // per-launch timing of the traversal kernels
     std::vector<hipEvent_t> ev;
@@ -523,16 +650,16 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
             (void)hipEventRecord(e2, str);
             trace_s<<<grid_t, kBlk, 0, str>>>(view(s), st, parity, ovf);
             (void)hipEventRecord(e3, str);
-            k_wf_advance<<<1, 1, 0, str>>>(st, parity);
+            k_wf_advance<<<1, kSeg, 0, str>>>(st, parity);
             ext_ev.push_back({e0, e1});
             sh_ev.push_back({e2, e3});
             parity ^= 1;
         }
         if (hipGetLastError() != hipSuccess) { rc = -1; break; }
-        if (hipMemcpyAsync(h_cnt, st.ctl, 8, hipMemcpyDeviceToHost, str) != hipSuccess ||
+        if (hipMemcpyAsync(h_cnt, st.total, 4, hipMemcpyDeviceToHost, str) != hipSuccess ||
             hipStreamSynchronize(str) != hipSuccess) { rc = -1; break; }
-        if (h_cnt[0] == 0 && h_cnt[1] == 0) break;
-        if (it > (int64_t)a.spp * (kMaxDepth + 2) + 64) {  // cannot happen: each pixel needs <= spp*(kMaxDepth+1) iterations
+        if (h_cnt[0] == 0) break;
+        if (it > (int64_t)a.spp * (kMaxDepth + 2) + 64) {  // each pixel needs <= spp*(kMaxDepth+1) iterations
             set_error("wavefront: iteration bound exceeded");
             rc = -3;
             break;
@@ -569,7 +696,9 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
                     float* d_hits, int32_t* d_ids)
 {
-    auto fn = any ? k_intersect<true, kBlk, kSL> : k_intersect<false, kBlk, kSL>;
+    const bool wide = use_wide();
+    auto fn = wide ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<true, false, kBlk, kSL>)
+                   : (any ? k_intersect<false, true, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (n + kBlk - 1) / kBlk));
     size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);

@@ -80,6 +80,7 @@ struct TravStack {
 
 struct SceneView {
     const BvhNode* __restrict__ nodes;
+    const Bvh4Node* __restrict__ nodes4;
     const TriPre* __restrict__ tri_pre;
     const TriOrig* __restrict__ tri_orig;
     const float2* __restrict__ sincos;
@@ -90,61 +91,203 @@ struct TravCount {
     uint32_t nodes = 0, tris = 0;
 };
 
-// Closest hit.  Returns the original triangle index or -1; t/u/v of the hit.
+// Resumable traversal state of one lane (registers).
+struct TravState {
+    int node;   // next node (>=0 internal, <0 leaf = ~slot)
+    int sp;     // stack depth
+    int best;   // original triangle index of the current closest hit, -1 if none
+    float bt, bu, bv;
+};
+
+__device__ __forceinline__ void trav_init(TravState& ts, float tmax)
+{
+    ts.node = 0;
+    ts.sp = 0;
+    ts.best = -1;
+    ts.bt = tmax;
+    ts.bu = ts.bv = 0.0f;
+}
+
+// One traversal step: one internal node (both child boxes) or one leaf
+// triangle.  Returns true when the query is finished (stack empty, or the
+// first accepted hit of an any-hit query).
 template <bool ANY, bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step(const SceneView& sv, const TravRay& r, float tlo,
+                                          float tmin, float tmax, TravState& ts,
+                                          TravStack<BLOCK, SL>& st, TravCount& cnt)
+{
+    if (ts.node >= 0) {
+        const float4* p = reinterpret_cast<const float4*>(sv.nodes + ts.node);
+        float4 a = p[0], b = p[1], c = p[2];
+        int4 lk = reinterpret_cast<const int4*>(p)[3];
+        if (COUNT) ++cnt.nodes;
+        float tn0, tn1;
+        bool h0 = slab(r, a.x, a.y, a.z, a.w, b.x, b.y, tlo, ts.bt, tn0);
+        bool h1 = slab(r, b.z, b.w, c.x, c.y, c.z, c.w, tlo, ts.bt, tn1);
+        if (h0 && h1) {
+            int nearc = lk.x, farc = lk.y;
+            if (tn1 < tn0) { nearc = lk.y; farc = lk.x; }
+            st.push(ts.sp, farc);
+            ts.node = nearc;
+            return false;
+        }
+        if (h0 || h1) {
+            ts.node = h0 ? lk.x : lk.y;
+            return false;
+        }
+    } else {
+        const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + (~ts.node));
+        float4 a = p[0], b = p[1], c = p[2];
+        if (COUNT) ++cnt.tris;
+        float t, u, v;
+        if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
+                    t, u, v)) {
+            int id = __float_as_int(c.y);
+            if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                ts.bt = t;
+                ts.bu = u;
+                ts.bv = v;
+                ts.best = id;
+                if (ANY) return true;
+            }
+        }
+    }
+    if (ts.sp == 0) return true;
+    ts.node = st.pop(ts.sp);
+    return false;
+}
+
+__device__ __forceinline__ float exp_scale(uint32_t biased) { return __uint_as_float((biased & 0xFFu) << 23); }
+
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool leaf_tris(const SceneView& sv, const TravRay& r, float tmin,
+                                          float tmax, TravState& ts, uint32_t code,
+                                          TravCount& cnt)
+{
+    const uint32_t first = code & kLeafFirstMask;
+    const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
+    for (uint32_t k = 0; k < n; ++k) {
+        const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
+        float4 a = p[0], b = p[1], c = p[2];
+        if (COUNT) ++cnt.tris;
+        float t, u, v;
+        if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
+                    t, u, v)) {
+            int id = __float_as_int(c.y);
+            if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                ts.bt = t;
+                ts.bu = u;
+                ts.bv = v;
+                ts.best = id;
+                if (ANY) return true;
+            }
+        }
+    }
+    return false;
+}
+
+// One step over the 4-wide quantised BVH: one node (four child boxes decoded
+// as origin + q*2^e, slab distances t = q*(2^e/d) + (origin-o)/d, one fma per
+// plane) or one leaf (its triangle range).  Closest hit: hit children sorted
+// near to far (5-exchange network), nearest taken, others pushed far first.
+template <bool ANY, bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r, float tlo,
+                                           float tmin, float tmax, TravState& ts,
+                                           TravStack<BLOCK, SL>& st, TravCount& cnt)
+{
+    if (ts.node >= 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
+        uint4 A = p[0], B = p[1], C = p[2];
+        int4 L = reinterpret_cast<const int4*>(p)[3];
+        if (COUNT) ++cnt.nodes;
+        const float ax = exp_scale(A.w) * r.ix, bx = (__uint_as_float(A.x) - r.o.x) * r.ix;
+        const float ay = exp_scale(A.w >> 8) * r.iy, by = (__uint_as_float(A.y) - r.o.y) * r.iy;
+        const float az = exp_scale(A.w >> 16) * r.iz, bz = (__uint_as_float(A.z) - r.o.z) * r.iz;
+        const uint32_t mask = A.w >> 24;
+        float key[4];
+        int ch[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sh = 8 * k;
+            float t0x = __builtin_fmaf((float)((B.x >> sh) & 255u), ax, bx);
+            float t1x = __builtin_fmaf((float)((B.y >> sh) & 255u), ax, bx);
+            float t0y = __builtin_fmaf((float)((B.z >> sh) & 255u), ay, by);
+            float t1y = __builtin_fmaf((float)((B.w >> sh) & 255u), ay, by);
+            float t0z = __builtin_fmaf((float)((C.x >> sh) & 255u), az, bz);
+            float t1z = __builtin_fmaf((float)((C.y >> sh) & 255u), az, bz);
+            float tn = max3f(fminf(t0x, t1x), fminf(t0y, t1y), fmaxf(fminf(t0z, t1z), tlo));
+            float tf = min3f(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fminf(fmaxf(t0z, t1z), ts.bt));
+            bool hit = ((mask >> k) & 1u) && tn <= tf * kTfarSlack;
+            key[k] = hit ? tn : INFINITY;
+        }
+        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
+                 (key[3] != INFINITY);
+        if (nh > 0) {
+            if (!ANY) {
+#define TMPT_CSWAP(i, j)                                            \
+    if (key[j] < key[i]) {                                          \
+        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
+        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
+    }
+                TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
+#undef TMPT_CSWAP
+                // hits now occupy 0..nh-1, nearest first
+                if (nh > 3) st.push(ts.sp, ch[3]);
+                if (nh > 2) st.push(ts.sp, ch[2]);
+                if (nh > 1) st.push(ts.sp, ch[1]);
+                ts.node = ch[0];
+            } else {
+                int next = 0;
+                bool have = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (key[k] != INFINITY) {
+                        if (!have) {
+                            next = ch[k];
+                            have = true;
+                        } else {
+                            st.push(ts.sp, ch[k]);
+                        }
+                    }
+                }
+                ts.node = next;
+            }
+            return false;
+        }
+    } else {
+        if (leaf_tris<ANY, COUNT>(sv, r, tmin, tmax, ts, (uint32_t)ts.node, cnt)) return true;
+    }
+    if (ts.sp == 0) return true;
+    ts.node = st.pop(ts.sp);
+    return false;
+}
+
+template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step_w(const SceneView& sv, const TravRay& r, float tlo,
+                                            float tmin, float tmax, TravState& ts,
+                                            TravStack<BLOCK, SL>& st, TravCount& cnt)
+{
+    if (WIDE) return trav_step4<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
+    return trav_step<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
+}
+
+// Whole query in one call.  Returns the original triangle index or -1.
+template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
                                         float tmax, float& bt, float& bu, float& bv,
                                         TravStack<BLOCK, SL>& st, TravCount& cnt)
 {
-    int best = -1;
-    bt = tmax;
-    if (sv.n <= 0) return -1;
-    const float tlo = fminf(tmin, 0.0f);
-    int sp = 0;
-    int node = 0;
-    for (;;) {
-        if (node >= 0) {
-            const float4* p = reinterpret_cast<const float4*>(sv.nodes + node);
-            float4 a = p[0], b = p[1], c = p[2];
-            int4 lk = reinterpret_cast<const int4*>(p)[3];
-            if (COUNT) ++cnt.nodes;
-            float tn0, tn1;
-            bool h0 = slab(r, a.x, a.y, a.z, a.w, b.x, b.y, tlo, bt, tn0);
-            bool h1 = slab(r, b.z, b.w, c.x, c.y, c.z, c.w, tlo, bt, tn1);
-            if (h0 && h1) {
-                int nearc = lk.x, farc = lk.y;
-                if (tn1 < tn0) { nearc = lk.y; farc = lk.x; }
-                st.push(sp, farc);
-                node = nearc;
-            } else if (h0) {
-                node = lk.x;
-            } else if (h1) {
-                node = lk.y;
-            } else {
-                if (sp == 0) break;
-                node = st.pop(sp);
-            }
-        } else {
-            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + (~node));
-            float4 a = p[0], b = p[1], c = p[2];
-            if (COUNT) ++cnt.tris;
-            float t, u, v;
-            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
-                        t, u, v)) {
-                int id = __float_as_int(c.y);
-                if (t < bt || (t == bt && best >= 0 && id < best)) {
-                    bt = t;
-                    bu = u;
-                    bv = v;
-                    best = id;
-                    if (ANY) return best;
-                }
-            }
-            if (sp == 0) break;
-            node = st.pop(sp);
+    TravState ts;
+    trav_init(ts, tmax);
+    if (sv.n > 0) {
+        const float tlo = fminf(tmin, 0.0f);
+        while (!trav_step_w<WIDE, ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt)) {
         }
     }
-    return best;
+    bt = ts.bt;
+    bu = ts.bu;
+    bv = ts.bv;
+    return ts.best;
 }
 
 // pos and normal of an accepted hit (maths.cpp:375-377)
