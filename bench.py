@@ -219,7 +219,9 @@ def main() -> None:
                    "rays_per_step": rays // args.steps},
         "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity,
         "scene_init_s": round(init_s, 3), "bvh_build_ms": round(st0.build_ms, 2),
-        "bvh_depth": st0.bvh_depth,
+        "bvh": {"lbvh2_depth": st0.bvh_depth, "bvh4_nodes": st0.bvh4_nodes, "bvh4_depth": st0.bvh4_depth,
+                "leaf_max": st0.leaf_max, "builder": "ploc" if st0.builder_iters else "lbvh",
+                "ploc_iters": st0.builder_iters},
     }
     print(json.dumps(out), flush=True)
     scene.close()

@@ -73,6 +73,7 @@ typedef struct {
     uint64_t shadow_node_visits, shadow_tri_tests; /* shadow (any-hit) kernel, same flag */
     double build_ms;                 /* LBVH build of the scene */
     int32_t bvh_nodes, bvh_depth, n_tris, device;
+    int32_t bvh4_nodes, bvh4_depth, leaf_max, builder_iters; /* 4-wide tree; PLOC passes (0 = LBVH) */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */

@@ -93,6 +93,33 @@ def test_hitscene_vs_linear_scan(gpu, name):
     sc.close()
 
 
+def test_hitscene_nan_and_degenerate_rays(gpu):
+    """NaN rays (normalize of a zero vector, main.cpp:72) never hit in the
+    reference (every Moller-Trumbore comparison is false); rays along a face
+    plane, from a vertex, and zero-length directions behave as the oracle."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    nan = np.float32("nan")
+    c = ((bmin + bmax) / 2).astype(np.float32)
+    v = tris[5]
+    rays = np.array([
+        [*c, nan, nan, nan],
+        [*c, nan, 0.0, 1.0],
+        [nan, 0.0, 0.0, 0.0, 1.0, 0.0],
+        [*v[0], *((v[1] - v[0]) / np.linalg.norm(v[1] - v[0]))],   # along an edge
+        [*v[0], 0.0, 1.0, 0.0],                                     # from a vertex
+        [*c, 0.0, 0.0, 0.0],                                        # zero direction
+        [*(c + 100.0), -0.57735026, -0.57735026, -0.57735026],
+    ], np.float32)
+    ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_LINEAR)
+    oids, ohits = osc.hit_batch(rays, 0.001, 1.0e7)
+    assert list(ids[:3]) == [-1, -1, -1]
+    assert np.array_equal(ids, oids)
+    h = ids >= 0
+    assert np.array_equal(hits[h].view(np.uint32), ohits[h].view(np.uint32))
+    sc.close()
+
+
 def test_hitscene_reference_contract(gpu):
     """Single-ray form returns 1 / -1 like scene.cpp:132-139."""
     tris, bmin, bmax, sc = _scene("cube.obj")

@@ -1,6 +1,13 @@
-"""Interleaved A/B of traversal-kernel variants (TMPT_TUNE) in ONE process on
-the bench frame (sponza stand-in 1920x1080, pixel seeding).  Prints per-variant
-MRays/s (median over rounds) and the extend/shadow kernel times."""
+"""Interleaved A/B of build/traversal variants in ONE process on the bench frame
+(sponza stand-in 1920x1080, pixel seeding; MI355X_MICROARCH-style rule: compare
+variants in one process, interleaved rounds).
+
+  python tools/tune.py "TMPT_BUILDER=lbvh;TMPT_BUILDER=ploc,TMPT_PLOC_R=16" [spp] [rounds]
+
+Each variant is a comma list of env assignments.  Build-time keys
+(TMPT_BUILDER, TMPT_LEAF_MAX, TMPT_PLOC_R) select a scene built once per
+distinct setting; render-time keys (TMPT_TUNE, TMPT_BVH) are set per render.
+Every variant's image must equal the first one's (bit-exact contract)."""
 import os
 import sys
 import time
@@ -13,26 +20,64 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-variants = sys.argv[1].split(";") if len(sys.argv) > 1 else ["32,8,16"]
+BUILD_KEYS = ("TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R")
+RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH")
+
+variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+scene_name = os.environ.get("TUNE_SCENE", "sponza")
 W, H = 1920, 1080
-tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
-cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
-sc = tm.Scene(tris)
+path = gen_standin_sponza.ensure() if scene_name == "sponza" else os.path.join(ROOT, "data", scene_name)
+tris, bmin, bmax = tm.load_scene(path)
+cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=scene_name == "sponza")
+
+
+def parse(v):
+    d = {}
+    for kv in filter(None, v.split(",")):
+        k, _, val = kv.partition("=")
+        d[k.strip()] = val.strip()
+    return d
+
+
+scenes = {}
+
+
+def scene_for(env):
+    key = tuple((k, env.get(k)) for k in BUILD_KEYS)
+    if key not in scenes:
+        for k in BUILD_KEYS:
+            os.environ.pop(k, None)
+            if env.get(k) is not None:
+                os.environ[k] = env[k]
+        sc = tm.Scene(tris)
+        st = sc.stats()
+        print(f"scene {dict(key)}: build {st.build_ms:.1f} ms, bvh4 nodes {st.bvh4_nodes}, depth4 "
+              f"{st.bvh4_depth}, ploc iters {st.builder_iters}", flush=True)
+        scenes[key] = sc
+    return scenes[key]
+
+
 res = {v: [] for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        os.environ["TMPT_TUNE"] = v
+        env = parse(v)
+        sc = scene_for(env)
+        for k in RENDER_KEYS:
+            os.environ.pop(k, None)
+            if env.get(k) is not None:
+                os.environ[k] = env[k]
         t0 = time.perf_counter()
         img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_PIXEL)
         dt = time.perf_counter() - t0
         st = sc.stats()
         if ref is None:
             ref = img
-        assert np.array_equal(img, ref), v
+        assert np.array_equal(img, ref), f"variant {v!r} changed the image"
         res[v].append((rays / dt / 1e6, st.extend_ms, st.shadow_ms, dt * 1e3))
 for v, xs in res.items():
     a = np.array(xs)
-    print(f"{v:>12}: {np.median(a[:,0]):8.1f} MRays/s  extend {np.median(a[:,1]):7.1f} ms  shadow {np.median(a[:,2]):7.1f} ms  frame {np.median(a[:,3]):7.1f} ms", flush=True)
+    print(f"{v or 'default':>48}: {np.median(a[:, 0]):8.1f} MRays/s  extend {np.median(a[:, 1]):7.1f} ms  "
+          f"shadow {np.median(a[:, 2]):7.1f} ms  frame {np.median(a[:, 3]):7.1f} ms", flush=True)

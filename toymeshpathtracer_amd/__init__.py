@@ -91,7 +91,9 @@ class _Stats(ctypes.Structure):
                 ("shadow_node_visits", ctypes.c_uint64), ("shadow_tri_tests", ctypes.c_uint64),
                 ("build_ms", ctypes.c_double), ("bvh_nodes", ctypes.c_int32),
                 ("bvh_depth", ctypes.c_int32), ("n_tris", ctypes.c_int32),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("bvh4_nodes", ctypes.c_int32),
+                ("bvh4_depth", ctypes.c_int32), ("leaf_max", ctypes.c_int32),
+                ("builder_iters", ctypes.c_int32)]
 
 
 def _sig(name, res, args):
@@ -243,6 +245,10 @@ class RenderStats:
     bvh_depth: int
     n_tris: int
     device: int
+    bvh4_nodes: int
+    bvh4_depth: int
+    leaf_max: int
+    builder_iters: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

@@ -271,6 +271,10 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->bvh_depth = s.max_depth;
     o->n_tris = s.n;
     o->device = s.device;
+    o->bvh4_nodes = s.n_nodes4;
+    o->bvh4_depth = s.depth4;
+    o->leaf_max = s.leaf_max;
+    o->builder_iters = s.ploc_iters;
     return 0;
 }
 

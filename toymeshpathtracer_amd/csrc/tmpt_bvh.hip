@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <string>
 #include <chrono>
 #include <cmath>
 #include <mutex>
@@ -313,6 +314,132 @@ __global__ void __launch_bounds__(kBlock) k_assemble(const int2* __restrict__ ch
     nodes[i].d = make_int4(c.x, c.y, depth[i], 0);
 }
 
+// ---------------------------------------------------------------- PLOC
+// Parallel Locally-Ordered Clustering (Meister & Bittner, TVCG 2018) over the
+// Morton order: every cluster finds its nearest neighbour (smallest union
+// surface area) within +-r positions; mutual pairs merge into a new node; the
+// survivors are compacted in order.  Produces SAH-grade trees from the same
+// sorted keys as the LBVH.  Nodes are numbered in creation order (children
+// before parents), the root is the last one.
+__device__ __forceinline__ float half_area(float lx, float ly, float lz, float hx, float hy, float hz)
+{
+    float dx = hx - lx, dy = hy - ly, dz = hz - lz;
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_init(int32_t n, Soa6 leaf, const uint32_t* __restrict__ vals,
+                                                      int32_t* __restrict__ cid, Soa6 cb)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    int o = (int)vals[i];
+    cid[i] = ~i;
+    cb.lx[i] = leaf.lx[o]; cb.ly[i] = leaf.ly[o]; cb.lz[i] = leaf.lz[o];
+    cb.hx[i] = leaf.hx[o]; cb.hy[i] = leaf.hy[o]; cb.hz[i] = leaf.hz[o];
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_nn(int32_t N, int r, Soa6 cb, int32_t* __restrict__ nn)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    const float lx = cb.lx[i], ly = cb.ly[i], lz = cb.lz[i], hx = cb.hx[i], hy = cb.hy[i], hz = cb.hz[i];
+    float best = INFINITY;
+    int bj = -1;
+    const int j0 = max(0, i - r), j1 = min(N - 1, i + r);
+    for (int j = j0; j <= j1; ++j) {
+        if (j == i) continue;
+        float d = half_area(fminf(lx, cb.lx[j]), fminf(ly, cb.ly[j]), fminf(lz, cb.lz[j]),
+                            fmaxf(hx, cb.hx[j]), fmaxf(hy, cb.hy[j]), fmaxf(hz, cb.hz[j]));
+        if (d < best) {  // ascending j: ties keep the lower index
+            best = d;
+            bj = j;
+        }
+    }
+    nn[i] = bj;
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_merge(int32_t N, const int32_t* __restrict__ nn,
+                                                       int32_t* __restrict__ cid, Soa6 cb,
+                                                       uint32_t* __restrict__ valid, int2* __restrict__ child,
+                                                       Soa6 ib, int32_t* __restrict__ size,
+                                                       int32_t* __restrict__ iter, int it,
+                                                       uint32_t* __restrict__ counter)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    int j = nn[i];
+    bool mutual = j >= 0 && nn[j] == i;
+    if (mutual && i < j) {
+        int k = (int)atomicAdd(counter, 1u);
+        int c0 = cid[i], c1 = cid[j];
+        child[k] = make_int2(c0, c1);
+        float lx = fminf(cb.lx[i], cb.lx[j]), ly = fminf(cb.ly[i], cb.ly[j]), lz = fminf(cb.lz[i], cb.lz[j]);
+        float hx = fmaxf(cb.hx[i], cb.hx[j]), hy = fmaxf(cb.hy[i], cb.hy[j]), hz = fmaxf(cb.hz[i], cb.hz[j]);
+        ib.lx[k] = lx; ib.ly[k] = ly; ib.lz[k] = lz; ib.hx[k] = hx; ib.hy[k] = hy; ib.hz[k] = hz;
+        size[k] = (c0 < 0 ? 1 : size[c0]) + (c1 < 0 ? 1 : size[c1]);
+        iter[k] = it;
+        cid[i] = k;
+        cb.lx[i] = lx; cb.ly[i] = ly; cb.lz[i] = lz; cb.hx[i] = hx; cb.hy[i] = hy; cb.hz[i] = hz;
+        valid[i] = 1;
+    } else {
+        valid[i] = (mutual && i > j) ? 0u : 1u;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_compact(int32_t N, const uint32_t* __restrict__ valid,
+                                                         const uint32_t* __restrict__ pos,
+                                                         const int32_t* __restrict__ cid, Soa6 cb,
+                                                         int32_t* __restrict__ cid2, Soa6 cb2)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N || !valid[i]) return;
+    uint32_t d = pos[i];
+    cid2[d] = cid[i];
+    cb2.lx[d] = cb.lx[i]; cb2.ly[d] = cb.ly[i]; cb2.lz[d] = cb.lz[i];
+    cb2.hx[d] = cb.hx[i]; cb2.hy[d] = cb.hy[i]; cb2.hz[d] = cb.hz[i];
+}
+
+// Leaf renumbering so every subtree covers a contiguous slot range (needed by
+// multi-triangle leaves): top-down offsets, one launch per PLOC iteration in
+// reverse (a node's parent was created in a later iteration).
+__global__ void __launch_bounds__(kBlock) k_ploc_offsets(int32_t m, int it, const int32_t* __restrict__ iter,
+                                                         const int2* __restrict__ child,
+                                                         const int32_t* __restrict__ size,
+                                                         int32_t* __restrict__ off,
+                                                         uint32_t* __restrict__ new_slot)
+{
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m || iter[k] != it) return;
+    int o = off[k];
+    int2 c = child[k];
+    int s0 = c.x < 0 ? 1 : size[c.x];
+    if (c.x >= 0) off[c.x] = o; else new_slot[~c.x] = (uint32_t)o;
+    if (c.y >= 0) off[c.y] = o + s0; else new_slot[~c.y] = (uint32_t)(o + s0);
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_relabel(int32_t m, int2* __restrict__ child,
+                                                         const int32_t* __restrict__ off,
+                                                         const int32_t* __restrict__ size,
+                                                         int2* __restrict__ range,
+                                                         const uint32_t* __restrict__ new_slot)
+{
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    int2 c = child[k];
+    if (c.x < 0) c.x = ~(int)new_slot[~c.x];
+    if (c.y < 0) c.y = ~(int)new_slot[~c.y];
+    child[k] = c;
+    range[k] = make_int2(off[k], off[k] + size[k] - 1);
+}
+
+__global__ void __launch_bounds__(kBlock) k_ploc_vals(int32_t n, const uint32_t* __restrict__ new_slot,
+                                                      const uint32_t* __restrict__ vals,
+                                                      uint32_t* __restrict__ vals2)
+{
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) vals2[new_slot[i]] = vals[i];
+}
+
 // ---------------------------------------------------------------- BVH4Q collapse
 __device__ __forceinline__ void node_or_leaf_box(int c, const Soa6& leaf,
                                                  const uint32_t* __restrict__ vals, const Soa6& ib,
@@ -523,7 +650,9 @@ int build_lbvh(Scene& s, const float* d_tris9)
             std::swap(vi, vo);
         }
         // sorted (ki, vi)
-        k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, vi, s.tri_pre);
+        const char* bname = getenv("TMPT_BUILDER");
+        const bool ploc = !(bname && std::string(bname) == "lbvh") && n > 1;
+        s.has_bvh2 = !ploc;
         if (n == 1) {
             k_single<<<1, 1, 0, st>>>(leaf, s.nodes);
             s.max_depth = 0;
@@ -543,19 +672,89 @@ int build_lbvh(Scene& s, const float* d_tris9)
                 k_refit_level<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, L, leaf, vi, ib);
             k_assemble<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, leaf, vi, ib, s.nodes);
         }
-        // BVH2 -> BVH4Q, top-down, one launch per level
+        // binary tree the BVH4Q is collapsed from: the LBVH, or a PLOC tree
+        const int2* tchild = child;
+        const int2* trange = range;
+        Soa6 tib = ib;
+        const uint32_t* tvals = vi;
+        int troot = n == 1 ? ~0 : 0;
+        if (ploc) {
+            int r = 24;
+            if (const char* e = getenv("TMPT_PLOC_R")) r = std::max(1, std::min(256, atoi(e)));
+            int32_t* cidA = (int32_t*)alloc(nn * 4);
+            int32_t* cidB = (int32_t*)alloc(nn * 4);
+            float* cbAb = (float*)alloc(6 * nn * 4);
+            float* cbBb = (float*)alloc(6 * nn * 4);
+            int32_t* nnb = (int32_t*)alloc(nn * 4);
+            uint32_t* valid = (uint32_t*)alloc(nn * 4);
+            uint32_t* pos = (uint32_t*)alloc(nn * 4);
+            int2* pchild = (int2*)alloc(mm * sizeof(int2));
+            int2* prange = (int2*)alloc(mm * sizeof(int2));
+            float* pibb = (float*)alloc(6 * mm * 4);
+            int32_t* psize = (int32_t*)alloc(mm * 4);
+            int32_t* piter = (int32_t*)alloc(mm * 4);
+            int32_t* poff = (int32_t*)alloc(mm * 4);
+            uint32_t* new_slot = (uint32_t*)alloc(nn * 4);
+            uint32_t* pvals = (uint32_t*)alloc(nn * 4);
+            uint32_t* pcounter = (uint32_t*)alloc(4);
+            if (!cidA || !cidB || !cbAb || !cbBb || !nnb || !valid || !pos || !pchild || !prange || !pibb ||
+                !psize || !piter || !poff || !new_slot || !pvals || !pcounter) {
+                set_error("build: out of device memory (PLOC)");
+                rc = -1;
+                break;
+            }
+            auto soa = [](float* b, size_t k) { return Soa6{b, b + k, b + 2 * k, b + 3 * k, b + 4 * k, b + 5 * k}; };
+            Soa6 cbA = soa(cbAb, nn), cbB = soa(cbBb, nn), pib = soa(pibb, mm);
+            if (hipMemsetAsync(pcounter, 0, 4, st) != hipSuccess || hipMemsetAsync(poff, 0, mm * 4, st) != hipSuccess) {
+                rc = -1;
+                break;
+            }
+            k_ploc_init<<<blocks_for(n, kBlock), kBlock, 0, st>>>(n, leaf, vi, cidA, cbA);
+            int N = n, it = 0;
+            while (N > 1) {
+                k_ploc_nn<<<blocks_for(N, kBlock), kBlock, 0, st>>>(N, r, cbA, nnb);
+                k_ploc_merge<<<blocks_for(N, kBlock), kBlock, 0, st>>>(N, nnb, cidA, cbA, valid, pchild, pib,
+                                                                       psize, piter, it, pcounter);
+                uint32_t tail[2];
+                if (hipMemcpyAsync(pos, valid, (size_t)N * 4, hipMemcpyDeviceToDevice, st) != hipSuccess) { rc = -1; break; }
+                k_scan_1block<<<1, 1024, 0, st>>>(pos, N);
+                if (hipMemcpyAsync(&tail[0], pos + N - 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipMemcpyAsync(&tail[1], valid + N - 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }
+                k_ploc_compact<<<blocks_for(N, kBlock), kBlock, 0, st>>>(N, valid, pos, cidA, cbA, cidB, cbB);
+                std::swap(cidA, cidB);
+                std::swap(cbA, cbB);
+                int next = (int)(tail[0] + tail[1]);
+                if (next >= N) { set_error("build: PLOC made no progress"); rc = -2; break; }
+                N = next;
+                ++it;
+            }
+            if (rc) break;
+            for (int k = it - 1; k >= 0; --k)
+                k_ploc_offsets<<<blocks_for(m, kBlock), kBlock, 0, st>>>(m, k, piter, pchild, psize, poff, new_slot);
+            k_ploc_relabel<<<blocks_for(m, kBlock), kBlock, 0, st>>>(m, pchild, poff, psize, prange, new_slot);
+            k_ploc_vals<<<blocks_for(n, kBlock), kBlock, 0, st>>>(n, new_slot, vi, pvals);
+            tchild = pchild;
+            trange = prange;
+            tib = pib;
+            tvals = pvals;
+            troot = m - 1;  // the last merge creates the root
+            s.ploc_iters = it;
+        }
+        k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, tvals, s.tri_pre);
+        // binary tree -> BVH4Q, top-down, one launch per level
         int leaf_max = 2;
         if (const char* e = getenv("TMPT_LEAF_MAX")) leaf_max = std::max(1, std::min(kLeafMaxTris, atoi(e)));
         s.leaf_max = leaf_max;
-        int2 root = make_int2(n == 1 ? ~0 : 0, 0);
+        int2 root = make_int2(troot, 0);
         uint32_t hc[2] = {1u, 0u};
         if (hipMemcpyAsync(fr0, &root, sizeof(root), hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemcpyAsync(c4, hc, sizeof(hc), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
         int nf = 1, levels = 0;
         int2 *fa = fr0, *fb = fr1;
         while (nf > 0) {
-            k_bvh4_level<<<blocks_for(nf, kBlock), kBlock, 0, st>>>(child, range, leaf, vi, ib, fa, nf, fb,
-                                                                    c4, s.nodes4, leaf_max);
+            k_bvh4_level<<<blocks_for(nf, kBlock), kBlock, 0, st>>>(tchild, trange, leaf, tvals, tib, fa, nf,
+                                                                    fb, c4, s.nodes4, leaf_max);
             ++levels;
             if (hipMemcpyAsync(hc, c4, sizeof(hc), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }

@@ -80,7 +80,8 @@ struct Scene {
     int32_t max_depth = 0;  // of the LBVH
     BvhNode* nodes = nullptr;
     Bvh4Node* nodes4 = nullptr;
-    int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0;
+    int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
+    bool has_bvh2 = true;  // the LBVH2 (A/B layout) matches tri_pre only for the LBVH builder
     TriPre* tri_pre = nullptr;
     TriOrig* tri_orig = nullptr;
     const float2* sincos = nullptr;  // borrowed from the per-device table

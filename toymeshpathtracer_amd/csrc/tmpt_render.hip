@@ -198,7 +198,8 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
 // wave appends and the consumers' chunk reservations spread over kSeg words
 // instead of serialising on one (MI355X_MICROARCH.md: one word saturates at
 // ~88 atomics/us).
-constexpr int kSeg = 64;
+constexpr int kSeg = 64;  // == wave width: one lane probes one segment
+static_assert(kSeg == 64, "segment probing maps segments to the 64 lanes of a wave");
 constexpr int kCtr = 16;  // words between counters (64 B)
 constexpr uint32_t kChunk = 64;  // queue entries a wave reserves per atomic
 constexpr uint32_t kSkip = 0x80000000u;  // queue-entry flag: path stopped at kMaxDepth
@@ -221,6 +222,7 @@ struct WfState {
     uint32_t* head_e;  // fetch heads
     uint32_t* head_s;
     uint32_t* total;   // [0]: entries of the queue the next iteration consumes
+    uint32_t* iter_log;  // optional (TMPT_ITER_LOG): per-iteration queue sizes
     unsigned long long* tot;  // [0] extend rays [1] shadow rays [2,3] extend node/tri visits [4,5] shadow
     int64_t P;
     uint32_t seg_cap;
@@ -260,8 +262,9 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 // segment; exhausted segments are skipped, starting from the wave's own, so
 // waves work on nearby pixels and the heads see few atomics.  Lanes run
 // STEPS traversal steps between refill checks.
-template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 16>
-__global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int parity,
+template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 16, int MINW = 1,
+          int PROBE = 1>
+__global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState s, int parity,
                                                     uint32_t* __restrict__ ovf)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
@@ -276,31 +279,48 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
     const f3 ldir = light_dir();
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     const uint32_t wave_gid = (uint32_t)(gtid >> 6);
-    uint32_t seg = wave_gid % kSeg, seg_left = kSeg;  // segments not yet found exhausted
-    uint32_t res = 0, res_end = 0;                    // reservation [res, res_end) of queue positions
+    uint32_t seg = wave_gid % kSeg;  // current segment; starts spread over the frame
+    bool probe = false, drained = false;
+    uint32_t walked = 0;
+    uint32_t res = 0, res_end = 0;          // reservation [res, res_end) of queue positions
     bool active = false;
     uint32_t p = 0;
+    uint32_t steps = 0, max_steps = 0;  // COUNT builds: longest query of this lane
     TravRay r;
     TravState ts;
     for (;;) {
         uint64_t idle = __ballot(!active);
         uint32_t nidle = (uint32_t)__popcll(idle);
-        if (nidle >= (uint32_t)REFILL && (res < res_end || seg_left > 0)) {
-            while (res >= res_end && seg_left > 0) {  // renew the reservation (wave-uniform)
-                uint32_t c = counts[seg * kCtr];
-                uint32_t h = __hip_atomic_load(&heads[seg * kCtr], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t b = c;
-                if (h < c) {
-                    if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
-                    b = (uint32_t)__shfl((int)b, 0);
+        if (nidle >= (uint32_t)REFILL && (res < res_end || !drained)) {
+            while (res >= res_end && !drained) {  // renew the reservation (wave-uniform)
+                if (probe) {
+                    // the current segment ran dry: lane j probes segment j, so ONE round
+                    // trip finds every segment with entries left (or proves the queue empty)
+                    const uint32_t cj = counts[lane_id() * kCtr];
+                    const uint32_t hj = __hip_atomic_load(&heads[lane_id() * kCtr], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t open = __ballot(hj < cj);
+                    if (open == 0) {
+                        drained = true;
+                        break;
+                    }
+                    // first open segment after the current one (rotate the mask)
+                    const uint64_t rot = (open >> seg) | (seg ? (open << (64 - seg)) : 0ull);
+                    seg = (seg + (uint32_t)(__ffsll((unsigned long long)rot) - 1)) & 63u;
+                    probe = false;
                 }
+                const uint32_t c = counts[seg * kCtr];
+                uint32_t b = 0;
+                if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
+                b = (uint32_t)__shfl((int)b, 0);
                 if (b < c) {
                     res = seg * s.seg_cap + b;
                     res_end = seg * s.seg_cap + min(b + kChunk, c);
-                } else {
-                    seg = seg + 1 == kSeg ? 0 : seg + 1;
-                    --seg_left;
+                } else if (PROBE) {
+                    probe = true;
+                } else {  // sequential walk: try the next segment, give up after all 64
+                    seg = (seg + 1) & 63u;
+                    if (++walked == kSeg) drained = true;
                 }
             }
             uint32_t take = min(nidle, res_end - res);
@@ -319,24 +339,31 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
                     }
                     r = make_trav_ray(o, d);
                     trav_init(ts, kMaxT);
-                    active = true;
                     ++traced;
+                    steps = 0;
+                    if (!ray_has_nan(o, d)) {
+                        active = true;
+                    } else if (!ANY) {  // provably no hit (ray_has_nan): a counted miss
+                        s.hid[p] = -1;
+                    }
                 }
             }
             res += take;
         }
         if (!__any(active)) {
-            if (res >= res_end && seg_left == 0) break;
+            if (res >= res_end && drained) break;
             continue;
         }
         if (active) {
             bool done = false;
             for (int k = 0; k < STEPS; ++k) {
                 done = trav_step_w<WIDE, ANY, COUNT>(sv, r, 0.0f, kMinT, kMaxT, ts, st, cnt);
+                if (COUNT) ++steps;
                 if (done) break;
             }
             if (done) {
                 active = false;
+                if (COUNT) max_steps = max(max_steps, steps);
                 if (ANY) {
                     if (ts.best >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
                 } else {
@@ -356,6 +383,10 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
             atomicAdd(&s.tot[ANY ? 4 : 2], (unsigned long long)nv);
             atomicAdd(&s.tot[ANY ? 5 : 3], (unsigned long long)nt);
         }
+    }
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) max_steps = max(max_steps, (uint32_t)__shfl_xor((int)max_steps, off));
+        if (lane_id() == 0) atomicMax(&s.tot[ANY ? 7 : 6], (unsigned long long)max_steps);
     }
 }
 
@@ -432,10 +463,18 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
 
 // after the extend of `parity` was consumed: zero its counts and the heads;
 // publish the size of the next queue for the host's termination check
-__global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity)
+__global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int it)
 {
     int j = threadIdx.x;
     uint32_t next = s.cnt[parity ^ 1][j * kCtr];
+    if (s.iter_log) {  // debug: rays of this iteration's extend (consumed queue) and shadow
+        uint32_t e = wave_sum(s.cnt[parity][j * kCtr]);
+        uint32_t sh = wave_sum(s.cnt_s[j * kCtr]);
+        if (j == 0) {
+            s.iter_log[2 * it] = e;
+            s.iter_log[2 * it + 1] = sh;
+        }
+    }
     s.cnt[parity][j * kCtr] = 0;
     s.cnt_s[j * kCtr] = 0;
     s.head_e[j * kCtr] = 0;
@@ -561,21 +600,22 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     int sl = kSL;
     // TMPT_TUNE=<sl>,<steps>,<refill>: tuning variants of the traversal kernels
     if (const char* tune = getenv("TMPT_TUNE")) {
-        int a0 = 0, a1 = 0, a2 = 0;
-        if (sscanf(tune, "%d,%d,%d", &a0, &a1, &a2) == 3 && !count) {
-#define TMPT_VARIANT(SL_, ST_, RF_)                                      \
-    if (wide && a0 == SL_ && a1 == ST_ && a2 == RF_) {                   \
-        trace_e = k_wf_trace<true, false, false, kBlk, SL_, ST_, RF_>;   \
-        trace_s = k_wf_trace<true, true, false, kBlk, SL_, ST_, RF_>;    \
-        sl = SL_;                                                        \
+        int a0 = 0, a1 = 0, a2 = 0, a3 = 1;
+        if (sscanf(tune, "%d,%d,%d,%d", &a0, &a1, &a2, &a3) >= 3 && !count) {
+#define TMPT_VARIANT(SL_, ST_, RF_, MW_)                                   \
+    if (wide && a0 == SL_ && a1 == ST_ && a2 == RF_ && a3 == MW_) {         \
+        trace_e = k_wf_trace<true, false, false, kBlk, SL_, ST_, RF_, MW_>; \
+        trace_s = k_wf_trace<true, true, false, kBlk, SL_, ST_, RF_, MW_>;  \
+        sl = SL_;                                                          \
     }
-            TMPT_VARIANT(16, 2, 16)
-            TMPT_VARIANT(16, 4, 16)
-            TMPT_VARIANT(16, 16, 16)
-            TMPT_VARIANT(32, 8, 16)
-            TMPT_VARIANT(16, 8, 8)
-            TMPT_VARIANT(16, 8, 32)
-            TMPT_VARIANT(24, 4, 16)
+            TMPT_VARIANT(16, 4, 16, 6)
+            TMPT_VARIANT(16, 4, 4, 1)
+            TMPT_VARIANT(16, 8, 16, 1)
+            if (wide && a0 == 16 && a1 == 4 && a2 == 16 && a3 == 100) {  // sequential segment walk
+                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 16, 1, 0>;
+                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 16, 1, 0>;
+                sl = 16;
+            }
 #undef TMPT_VARIANT
         }
     }
@@ -594,6 +634,9 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
            o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(qcap), o_q1 = take(qcap),
            o_qs = take(qcap), o_ctl = take(5 * ctr_words + 64), o_tot = take(16),
            o_ovf = take(ovf_words);
+    const bool log_iters = getenv("TMPT_ITER_LOG") != nullptr;
+    const int64_t max_log = (int64_t)a.spp * (kMaxDepth + 2) + 64 + 16;
+    size_t o_log = log_iters ? take(2 * (size_t)max_log) : 0;
     if (ensure_ws(s, words * 4)) return -1;
     uint32_t* w = (uint32_t*)s.ws;
     WfState st;
@@ -616,6 +659,7 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     st.head_s = st.head_e + ctr_words;
     st.total = st.head_s + ctr_words;
     st.tot = (unsigned long long*)(w + o_tot);
+    st.iter_log = log_iters ? w + o_log : nullptr;
     st.P = P;
     st.seg_cap = (uint32_t)seg_cap;
     uint32_t* ovf = w + o_ovf;
@@ -623,6 +667,7 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 
     TMPT_HIP(hipMemsetAsync(w + o_ctl, 0, (5 * ctr_words + 64) * 4, str));
     TMPT_HIP(hipMemsetAsync(st.tot, 0, 8 * sizeof(unsigned long long), str));
+    if (st.iter_log) TMPT_HIP(hipMemsetAsync(st.iter_log, 0, 8 * (size_t)max_log, str));
     k_wf_generate<kBlk><<<(int)((std::max<int64_t>(P, kSeg) + kBlk - 1) / kBlk), kBlk, 0, str>>>(a, st);
 
     // per-launch timing of the traversal kernels
@@ -650,7 +695,7 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
             (void)hipEventRecord(e2, str);
             trace_s<<<grid_t, kBlk, 0, str>>>(view(s), st, parity, ovf);
             (void)hipEventRecord(e3, str);
-            k_wf_advance<<<1, kSeg, 0, str>>>(st, parity);
+            k_wf_advance<<<1, kSeg, 0, str>>>(st, parity, (int)std::min<int64_t>(it, max_log - 1));
             ext_ev.push_back({e0, e1});
             sh_ev.push_back({e2, e3});
             parity ^= 1;
@@ -665,10 +710,17 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
             break;
         }
     }
-    unsigned long long tot[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rc == 0) {
         TMPT_HIP(hipMemcpyAsync(tot, st.tot, sizeof(tot), hipMemcpyDeviceToHost, str));
         TMPT_HIP(hipStreamSynchronize(str));
+        if (log_iters) {
+            std::vector<uint32_t> lg(2 * (size_t)std::min<int64_t>(it, max_log));
+            TMPT_HIP(hipMemcpy(lg.data(), st.iter_log, lg.size() * 4, hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < lg.size() / 2; ++k)
+                fprintf(stderr, "tmpt-iter %zu extend %u shadow %u\n", k, lg[2 * k], lg[2 * k + 1]);
+            if (count) fprintf(stderr, "tmpt-max-steps extend %llu shadow %llu\n", tot[6], tot[7]);
+        }
     }
     double ems = 0, sms = 0;
     for (auto& pr : ext_ev) { float ms = 0; (void)hipEventElapsedTime(&ms, pr.first, pr.second); ems += ms; }
@@ -696,6 +748,10 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
                     float* d_hits, int32_t* d_ids)
 {
+    if (!use_wide() && !s.has_bvh2) {
+        set_error("TMPT_BVH=2 needs a scene built with TMPT_BUILDER=lbvh");
+        return -22;
+    }
     const bool wide = use_wide();
     auto fn = wide ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<true, false, kBlk, kSL>)
                    : (any ? k_intersect<false, true, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
@@ -711,6 +767,10 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
 int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t* d_out,
            uint64_t* ray_count)
 {
+    if (!use_wide() && !s.has_bvh2) {
+        set_error("TMPT_BVH=2 needs a scene built with TMPT_BUILDER=lbvh");
+        return -22;
+    }
     RenderArgs a = make_args(cam, d);
     bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
     unsigned long long* d_counters = nullptr;

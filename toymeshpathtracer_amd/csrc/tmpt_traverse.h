@@ -271,6 +271,19 @@ __device__ __forceinline__ bool trav_step_w(const SceneView& sv, const TravRay& 
     return trav_step<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
 }
 
+// A ray with a NaN in its origin or direction can never be accepted by
+// Moller-Trumbore (det, u, v and t all become NaN and every comparison of
+// maths.cpp:345-371 is false), so the reference's HitScene returns -1 for it.
+// It arises when normalize(target - pos) meets a zero vector (main.cpp:72:
+// the random unit vector exactly cancels the normal).  Traversing it would
+// visit every node (NaN slab distances never cull), so it is answered as a
+// miss up front; it still counts as a ray.
+__device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
+{
+    return __builtin_isnan(o.x) | __builtin_isnan(o.y) | __builtin_isnan(o.z) | __builtin_isnan(d.x) |
+           __builtin_isnan(d.y) | __builtin_isnan(d.z);
+}
+
 // Whole query in one call.  Returns the original triangle index or -1.
 template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
@@ -279,7 +292,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
 {
     TravState ts;
     trav_init(ts, tmax);
-    if (sv.n > 0) {
+    if (sv.n > 0 && !ray_has_nan(r.o, r.d)) {
         const float tlo = fminf(tmin, 0.0f);
         while (!trav_step_w<WIDE, ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt)) {
         }
