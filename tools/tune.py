@@ -2,9 +2,9 @@
 (sponza stand-in 1920x1080, pixel seeding; MI355X_MICROARCH-style rule: compare
 variants in one process, interleaved rounds).
 
-  python tools/tune.py "TMPT_BUILDER=lbvh;TMPT_BUILDER=ploc,TMPT_PLOC_R=16" [spp] [rounds]
+  python tools/tune.py "TMPT_BUILDER=lbvh;TMPT_BUILDER=ploc&TMPT_PLOC_R=16;TMPT_TUNE=16,4,16,1" [spp] [rounds]
 
-Each variant is a comma list of env assignments.  Build-time keys
+Variants are separated by ';', env assignments within a variant by '&'.  Build-time keys
 (TMPT_BUILDER, TMPT_LEAF_MAX, TMPT_PLOC_R) select a scene built once per
 distinct setting; render-time keys (TMPT_TUNE, TMPT_BVH) are set per render.
 Every variant's image must equal the first one's (bit-exact contract)."""
@@ -35,7 +35,7 @@ cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=scene_name == "sponza")
 
 def parse(v):
     d = {}
-    for kv in filter(None, v.split(",")):
+    for kv in filter(None, v.split("&")):
         k, _, val = kv.partition("=")
         d[k.strip()] = val.strip()
     return d

@@ -190,7 +190,7 @@ __device__ __forceinline__ bool leaf_tris(const SceneView& sv, const TravRay& r,
 // as origin + q*2^e, slab distances t = q*(2^e/d) + (origin-o)/d, one fma per
 // plane) or one leaf (its triangle range).  Closest hit: hit children sorted
 // near to far (5-exchange network), nearest taken, others pushed far first.
-template <bool ANY, bool COUNT, int BLOCK, int SL>
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
 __device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r, float tlo,
                                            float tmin, float tmax, TravState& ts,
                                            TravStack<BLOCK, SL>& st, TravCount& cnt)
@@ -223,7 +223,7 @@ __device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r
         int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
                  (key[3] != INFINITY);
         if (nh > 0) {
-            if (!ANY) {
+            if (SORT) {
 #define TMPT_CSWAP(i, j)                                            \
     if (key[j] < key[i]) {                                          \
         float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
@@ -262,12 +262,12 @@ __device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r
     return false;
 }
 
-template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL>
+template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
 __device__ __forceinline__ bool trav_step_w(const SceneView& sv, const TravRay& r, float tlo,
                                             float tmin, float tmax, TravState& ts,
                                             TravStack<BLOCK, SL>& st, TravCount& cnt)
 {
-    if (WIDE) return trav_step4<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
+    if (WIDE) return trav_step4<ANY, COUNT, BLOCK, SL, SORT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
     return trav_step<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
 }
 
