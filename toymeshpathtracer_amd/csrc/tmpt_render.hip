@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 // waves work on nearby pixels and the heads see few atomics.  Lanes run
 // STEPS traversal steps between refill checks.
 template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 8, int MINW = 1,
-          int PROBE = 0, int SORT = !ANY>
+          int PROBE = 0, int SORT = !ANY, int VOTE = 1>
 __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState s, int parity,
                                                     uint32_t* __restrict__ ovf)
 {
@@ -357,9 +357,24 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
         if (active) {
             bool done = false;
             for (int k = 0; k < STEPS; ++k) {
-                done = trav_step_w<WIDE, ANY, COUNT, BLOCK, SL, (bool)SORT>(sv, r, 0.0f, kMinT, kMaxT, ts, st, cnt);
-                if (COUNT) ++steps;
-                if (done) break;
+                if (VOTE) {
+                    // one step kind per round: inner nodes or leaves, whichever more
+                    // lanes are waiting for, so each load issues with more lanes
+                    const uint64_t at_leaf = __ballot(!done && ts.node < 0);
+                    const uint64_t at_node = __ballot(!done && ts.node >= 0);
+                    if (at_leaf == 0 && at_node == 0) break;
+                    const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
+                    if (!done && (ts.node < 0) == leaf_round) {
+                        done = trav_step_w<WIDE, ANY, COUNT, BLOCK, SL, (bool)SORT>(sv, r, 0.0f, kMinT, kMaxT, ts,
+                                                                                 st, cnt);
+                        if (COUNT) ++steps;
+                    }
+                } else {
+                    done = trav_step_w<WIDE, ANY, COUNT, BLOCK, SL, (bool)SORT>(sv, r, 0.0f, kMinT, kMaxT, ts, st,
+                                                                             cnt);
+                    if (COUNT) ++steps;
+                    if (done) break;
+                }
             }
             if (done) {
                 active = false;
@@ -608,21 +623,21 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
         trace_s = k_wf_trace<true, true, false, kBlk, SL_, ST_, RF_, MW_>;  \
         sl = SL_;                                                          \
     }
-            TMPT_VARIANT(16, 2, 16, 1)
-            TMPT_VARIANT(16, 8, 16, 1)
-            TMPT_VARIANT(16, 16, 16, 1)
-            TMPT_VARIANT(16, 4, 16, 1)
-            TMPT_VARIANT(16, 4, 32, 1)
-            TMPT_VARIANT(16, 8, 8, 1)
-            TMPT_VARIANT(16, 4, 16, 6)
-            TMPT_VARIANT(32, 4, 16, 1)
-            TMPT_VARIANT(8, 4, 16, 1)
-            if (wide && a0 == 16 && a1 == 4 && a2 == 16 && a3 == 200) {  // nearest-first any-hit
-                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 16, 1, 0, 1>;
+            TMPT_VARIANT(16, 4, 8, 6)
+            TMPT_VARIANT(16, 4, 8, 8)
+            TMPT_VARIANT(8, 4, 8, 6)
+            TMPT_VARIANT(8, 4, 8, 8)
+            TMPT_VARIANT(24, 4, 8, 1)
+            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 0) {  // no vote (both step kinds per round)
+                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 8, 1, 0, 1, 0>;
+                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 0, 0, 0>;
             }
-            if (wide && a0 == 16 && a1 == 4 && a2 == 16 && a3 == 100) {  // probing segment fetch
-                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 16, 1, 1>;
-                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 16, 1, 1>;
+            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 200) {  // nearest-first any-hit
+                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 0, 1>;
+            }
+            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 100) {  // probing segment fetch
+                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 8, 1, 1>;
+                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 1>;
             }
 #undef TMPT_VARIANT
         }
