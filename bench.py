@@ -5,14 +5,14 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
 is launched by torch.distributed.run, one rank per GPU.  One *step* = one full
 frame of BASELINE.json configs[3]: sponza.obj 1920x1080, 64 spp (the
 deterministic stand-in scene, data/gen_standin_sponza.py; the real sponza.obj
-is absent from the reference), pixel-mode seeding, wavefront engine.  The frame
+is absent from the reference), pixel-mode seeding, persistent path engine.  The frame
 is sharded over the N GPUs in 16-row bands dealt round-robin (total work fixed:
 strong scaling); each rank renders its bands straight into a device tensor and
 one RCCL gather over xGMI assembles the image on rank 0 -- inside the timed
 region.  value = all rays of all ranks / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
-  roofline      dominant kernel (extend = closest-hit traversal): algorithmic
+  roofline      dominant kernel (k_path: all queries of the frame): algorithmic
                 bytes per launch (B_ray = 32 + 16 + 64*N_node +
                 36*N_tri, N_node/N_tri measured by an instrumented run of the same
                 kernel on the same frame at reduced spp) / its mean launch time,
@@ -75,11 +75,14 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
-    ap.add_argument("--engine", default="wavefront", choices=["wavefront", "mega"])
+    ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
     ap.add_argument("--cpu-row-step", type=int, default=64, help="CPU baseline: every k-th row")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--save", default="", help="rank 0 writes the frame as PNG here")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path "
+                         "(ranks may share one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,14 +90,20 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1) if args.dist_backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     obj, W, H, SPP, sponza = CONFIGS[args.config]
     path = scene_path(obj)
-    engine = tm.ENGINE_WAVEFRONT if args.engine == "wavefront" else tm.ENGINE_MEGAKERNEL
+    engine = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT,
+              "mega": tm.ENGINE_MEGAKERNEL}[args.engine]
     tris, bmin, bmax = tm.load_scene(path)
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
     t0 = time.perf_counter()
@@ -106,7 +115,9 @@ def main() -> None:
     max_rows = max(len(r) for r in rows_of)
     my_rows = len(rows_of[rank])
     tile = torch.zeros((max_rows, W, 4), dtype=torch.uint8, device=dev)
-    gathered = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
+    gloo = world > 1 and args.dist_backend == "gloo"
+    gdev = torch.device("cpu") if gloo else dev
+    gathered = [torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)] if rank == 0 else None
     image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
 
     def step():
@@ -115,9 +126,10 @@ def main() -> None:
                                     out=tile.data_ptr())
         st = scene.stats()
         if world > 1:
-            dist.gather(tile, gathered, dst=0)
+            dist.gather(tile.cpu() if gloo else tile, gathered, dst=0)
         if rank == 0:  # de-interleave the bands into the frame, on the device
-            sharding.assemble(gathered if world > 1 else [tile], rows_of, image)
+            parts = [g.to(dev) for g in gathered] if gloo else (gathered if world > 1 else [tile])
+            sharding.assemble(parts, rows_of, image)
         return rays, st
 
     for _ in range(args.warmup):
@@ -143,10 +155,10 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.int64, device=dev)
+        r = torch.tensor([rays], dtype=torch.int64, device=gdev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
@@ -155,6 +167,8 @@ def main() -> None:
         scene.close()
         dist.destroy_process_group()
         return
+    if world > 1:
+        log(f"gathered frame: {world} ranks ({args.dist_backend}), {rays} rays")
 
     # ---- roofline of the dominant kernel (extend), from an instrumented run
     frame = image.cpu().numpy()
@@ -181,6 +195,21 @@ def main() -> None:
                 "shadow_bytes_per_ray": round(S_RAY + S_NODE * n_node_s + S_TRI * n_tri_s, 1),
                 "extend_ms_per_step": round(ext_ms / args.steps, 2),
                 "shadow_ms_per_step": round(sh_ms / args.steps, 2)}
+    elif engine == tm.ENGINE_PERSISTENT and cs.extend_rays and ext_launches:
+        # one launch per frame serves both query kinds: per-query averages over all of them
+        q = cs.extend_rays + cs.shadow_rays
+        n_node = cs.node_visits / q
+        n_tri = cs.tri_tests / q
+        b_ray = S_RAY + S_NODE * n_node + S_TRI * n_tri
+        per_launch_rays = (ext_rays + sh_rays) / ext_launches
+        avg_launch_ms = ext_ms / ext_launches
+        achieved = b_ray * per_launch_rays / (avg_launch_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_path (persistent: closest-hit + shadow queries + shading)",
+                "bytes_per_ray": round(b_ray, 1), "n_node_per_ray": round(n_node, 2),
+                "n_tri_per_ray": round(n_tri, 2), "avg_launch_ms": round(avg_launch_ms, 4),
+                "rays_per_launch": round(per_launch_rays, 1)}
 
     # ---- CPU baseline: the reference algorithm on this host, bounded row sample
     cpu = None

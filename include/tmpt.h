@@ -37,7 +37,9 @@ enum { TMPT_SEED_ROW = 0, TMPT_SEED_PIXEL = 1 };
 /* render engines */
 enum {
     TMPT_ENGINE_WAVEFRONT = 0,  /* generate/extend/shade/shadow kernels over compacted queues */
-    TMPT_ENGINE_MEGAKERNEL = 1  /* one lane per pixel (pixel mode) or per row (row mode) */
+    TMPT_ENGINE_MEGAKERNEL = 1, /* one lane per pixel (pixel mode) or per row (row mode) */
+    TMPT_ENGINE_PERSISTENT = 2  /* pixel mode: one persistent kernel per frame, lanes own pixels and
+                                   schedule extend / shadow / shade per wave (row mode: megakernel) */
 };
 
 /* render flags */

@@ -146,7 +146,7 @@ def test_row_mode_reproduces_reference_binary(gpu, name):
     sc.close()
 
 
-@pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+@pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL, tm.ENGINE_PERSISTENT])
 @pytest.mark.parametrize("name,w,h,spp", [("cube.obj", 640, 360, 4), ("suzanne.obj", 640, 360, 4),
                                           ("teapot.obj", 320, 180, 4)])
 def test_pixel_mode_matches_oracle(gpu, engine, name, w, h, spp):
@@ -161,7 +161,8 @@ def test_pixel_mode_matches_oracle(gpu, engine, name, w, h, spp):
     sc.close()
 
 
-def test_shards_assemble_to_full_frame(gpu):
+@pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_PERSISTENT])
+def test_shards_assemble_to_full_frame(gpu, engine):
     """Interleaved 16-row bands over 3 shards reassemble to the 1-shard frame."""
     tris, bmin, bmax, sc = _scene("teapot.obj")
     w, h, spp = 320, 180, 2
@@ -171,7 +172,7 @@ def test_shards_assemble_to_full_frame(gpu):
     total = 0
     for s in range(3):
         tile, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16, shard=s,
-                                 num_shards=3)
+                                 num_shards=3, engine=engine)
         ys = tm.tile_row_to_y(w, h, 16, s, 3)
         out[ys] = tile
         total += r
@@ -188,7 +189,8 @@ def test_sponza_standin_rows_match_oracle(gpu, sponza_path):
     with tm.Scene(tris) as sc:
         img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
         img2, rays2 = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
-    assert rays == rays2 and np.array_equal(img, img2)
+        img3, rays3 = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_PERSISTENT)
+    assert rays == rays2 == rays3 and np.array_equal(img, img2) and np.array_equal(img, img3)
     osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
     ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL, row_step=64)
     rows = np.arange(0, h, 64)
@@ -203,7 +205,8 @@ def test_full_size_teapot_engine_independence(gpu):
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT)
     b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_MEGAKERNEL)
-    assert ra == rb and np.array_equal(a, b)
+    c, rc = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_PERSISTENT)
+    assert ra == rb == rc and np.array_equal(a, b) and np.array_equal(a, c)
     osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
     ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL, row_step=48)
     rows = np.arange(0, h, 48)

@@ -28,12 +28,12 @@ import numpy as np
 
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
-    "SEED_ROW", "SEED_PIXEL", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "lib_path", "TmptError",
+    "SEED_ROW", "SEED_PIXEL", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
     "tile_rows", "tile_row_to_y",
 ]
 
 SEED_ROW, SEED_PIXEL = 0, 1
-ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL = 0, 1
+ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL, ENGINE_PERSISTENT = 0, 1, 2
 FLAG_OUT_DEVICE, FLAG_COUNT_VISITS = 1, 2
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -252,7 +252,7 @@ class RenderStats:
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
-          engine=ENGINE_WAVEFRONT, flags=0) -> _Desc:
+          engine=ENGINE_PERSISTENT, flags=0) -> _Desc:
     d = _Desc()
     d.width, d.height, d.spp, d.seed_mode = width, height, spp, seed_mode
     d.band_rows, d.shard, d.num_shards = band_rows, shard, num_shards
@@ -321,7 +321,7 @@ class Scene:
 
     # -- TraceImageBody over parallel_for (main.cpp:180-246, 329-331)
     def trace_image(self, camera: Camera, width: int, height: int, spp: int,
-                    seed_mode: int = SEED_ROW, engine: int = ENGINE_WAVEFRONT, band_rows: int = 0,
+                    seed_mode: int = SEED_ROW, engine: int = ENGINE_PERSISTENT, band_rows: int = 0,
                     shard: int = 0, num_shards: int = 1, count_visits: bool = False,
                     out=None) -> Tuple[np.ndarray, int]:
         """Render one shard.  Returns (rgba[tile_rows, width, 4] uint8, rays).

@@ -227,7 +227,8 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     if (d->spp < 1 || d->spp > 1024) return bad("tmpt_render: invalid samplesPerPixel");
     if (d->seed_mode != TMPT_SEED_ROW && d->seed_mode != TMPT_SEED_PIXEL)
         return bad("tmpt_render: invalid seed_mode");
-    if (d->engine != TMPT_ENGINE_WAVEFRONT && d->engine != TMPT_ENGINE_MEGAKERNEL)
+    if (d->engine != TMPT_ENGINE_WAVEFRONT && d->engine != TMPT_ENGINE_MEGAKERNEL &&
+        d->engine != TMPT_ENGINE_PERSISTENT)
         return bad("tmpt_render: invalid engine");
     if (d->num_shards > 1 && (d->shard < 0 || d->shard >= d->num_shards))
         return bad("tmpt_render: invalid shard");

@@ -1,5 +1,5 @@
 // tmpt_cli.cpp -- the reference's command line (main.cpp:248-345) over the C ABI:
-//   tmpt <width> <height> <spp> <objFile> [--seed row|pixel] [--engine wavefront|mega]
+//   tmpt <width> <height> <spp> <objFile> [--seed row|pixel] [--engine persistent|wavefront|mega]
 //        [--gpus N] [--device D] [--out output.png]
 // Defaults reproduce the reference: row seeding (main.cpp:204) and output.png.
 // Pixel seeding is what the wavefront engine parallelises; row mode runs the
@@ -25,7 +25,7 @@ int main(int argc, const char** argv)
 {
     if (argc < 5) {
         printf("Usage: tmpt [width] [height] [samplesPerPixel] [objFile] [--seed row|pixel] "
-               "[--engine wavefront|mega] [--gpus N] [--device D] [--out file.png]\n");
+               "[--engine persistent|wavefront|mega] [--gpus N] [--device D] [--out file.png]\n");
         return 1;
     }
     int w = atoi(argv[1]);
@@ -35,11 +35,15 @@ int main(int argc, const char** argv)
     int spp = atoi(argv[3]);
     if (spp < 1 || spp > 1024) { printf("ERROR: invalid samplesPerPixel argument '%s'\n", argv[3]); return 1; }
     const char* obj = argv[4];
-    int seed = TMPT_SEED_ROW, engine = TMPT_ENGINE_WAVEFRONT, gpus = 1, device = 0;
+    int seed = TMPT_SEED_ROW, engine = TMPT_ENGINE_PERSISTENT, gpus = 1, device = 0;
     const char* out = "output.png";
     for (int i = 5; i < argc; ++i) {
         if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strcmp(argv[++i], "pixel") ? TMPT_SEED_ROW : TMPT_SEED_PIXEL;
-        else if (!strcmp(argv[i], "--engine") && i + 1 < argc) engine = strcmp(argv[++i], "mega") ? TMPT_ENGINE_WAVEFRONT : TMPT_ENGINE_MEGAKERNEL;
+        else if (!strcmp(argv[i], "--engine") && i + 1 < argc) {
+            ++i;
+            engine = !strcmp(argv[i], "mega") ? TMPT_ENGINE_MEGAKERNEL
+                     : (!strcmp(argv[i], "wavefront") ? TMPT_ENGINE_WAVEFRONT : TMPT_ENGINE_PERSISTENT);
+        }
         else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--out") && i + 1 < argc) out = argv[++i];

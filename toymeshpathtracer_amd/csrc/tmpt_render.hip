@@ -498,6 +498,188 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
     if (j == 0) s.total[0] = next;
 }
 
+// ============================================================ persistent path engine
+// One persistent kernel per frame.  Every lane owns one pixel at a time and
+// runs its whole sample sequence (the RNG stream threads through the samples,
+// main.cpp:204-218); the extend / shadow / shade stages of the wavefront
+// engine become per-lane states scheduled inside the wave:
+//   * traversal rounds: lanes with a query in flight (closest hit or shadow,
+//     mixed) take STEPS steps; each step runs only the kind (inner node or
+//     leaf) that more lanes are waiting for;
+//   * shading rounds: once >= SHADE_MIN lanes have a finished query (or none is
+//     traversing), those lanes shade (Scatter / sky / backward recurrence /
+//     next camera sample / pixel write) and idle lanes take new pixels, a
+//     64-pixel reservation per atomic on segmented heads.
+// No per-bounce grid-wide synchronisation and no path state in HBM: light
+// scalars and the pending bounce ray live in LDS.
+struct PathCtl {
+    uint32_t* heads;  // kSeg pixel-segment heads, stride kCtr
+    uint32_t seg_cap;
+    int64_t P;
+};
+
+template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1>
+__global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, PathCtl pc,
+                                                uint32_t* __restrict__ out,
+                                                uint32_t* __restrict__ ovf,
+                                                unsigned long long* __restrict__ counters)
+{
+    __shared__ uint32_t s_stack[SL * BLOCK];
+    __shared__ float s_light[kMaxDepth * BLOCK];
+    __shared__ float s_next[6 * BLOCK];
+    const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    float* light = &s_light[threadIdx.x];
+    float* nxt = &s_next[threadIdx.x];
+    TravCount cnt;
+    uint32_t rays_e = 0, rays_s = 0;
+    const f3 ldir = light_dir();
+    const uint64_t lt = (1ull << lane_id()) - 1ull;
+    uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
+    uint32_t res = 0, res_end = 0;
+    bool exhausted = pc.P == 0;
+    bool has_pix = false, in_query = false, qany = false;
+    uint32_t pix = 0, rng = 0, smp = 0, depth = 0;
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    TravRay r;
+    TravState ts;
+    trav_init(ts, kMaxT);
+
+#define TMPT_START_QUERY(O_, D_, ANY_)                                         \
+    {                                                                          \
+        const f3 qo_ = (O_), qd_ = (D_);                                       \
+        r = make_trav_ray(qo_, qd_);                                           \
+        trav_init(ts, kMaxT);                                                  \
+        qany = (ANY_);                                                         \
+        if (qany) ++rays_s; else ++rays_e;                                     \
+        in_query = !ray_has_nan(qo_, qd_); /* NaN: a counted miss */           \
+    }
+#define TMPT_CAMERA_SAMPLE()                                                   \
+    {                                                                          \
+        const int lr_ = (int)(pix / (uint32_t)a.W);                            \
+        const int x_ = (int)(pix - (uint32_t)lr_ * (uint32_t)a.W);             \
+        f3 co_, cd_;                                                           \
+        camera_sample(a.cam, (uint32_t)x_, (uint32_t)tile_row_to_y(a, lr_),     \
+                      a.invW, a.invH, rng, co_, cd_);                          \
+        TMPT_START_QUERY(co_, cd_, false)                                      \
+    }
+
+    for (;;) {
+        const bool wants = has_pix ? !in_query : !exhausted;
+        const uint64_t need = __ballot(wants);
+        const uint64_t trav = __ballot(in_query);
+        if (need != 0 && (__popcll(need) >= SHADE_MIN || trav == 0)) {
+            // ---- new pixels for idle lanes (wave-uniform reservation)
+            const uint64_t nopix = __ballot(!has_pix && !exhausted);
+            if (nopix != 0) {
+                while (res >= res_end && !exhausted) {
+                    const int64_t lo = (int64_t)seg * pc.seg_cap;
+                    const int64_t left = pc.P - lo;
+                    const uint32_t c = left <= 0 ? 0u : (uint32_t)min<int64_t>(left, pc.seg_cap);
+                    uint32_t b = c;
+                    if (c != 0) {
+                        if (lane_id() == 0) b = atomicAdd(&pc.heads[seg * kCtr], kChunk);
+                        b = (uint32_t)__shfl((int)b, 0);
+                    }
+                    if (b < c) {
+                        res = (uint32_t)lo + b;
+                        res_end = (uint32_t)lo + min(b + kChunk, c);
+                    } else {
+                        seg = (seg + 1) & 63u;
+                        if (++walked == kSeg) exhausted = true;
+                    }
+                }
+                const uint32_t take = min((uint32_t)__popcll(nopix), res_end - res);
+                const uint32_t k = (uint32_t)__popcll(nopix & lt);
+                if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
+                    pix = res + k;
+                    has_pix = true;
+                    const int lr = (int)(pix / (uint32_t)a.W);
+                    const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
+                    rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
+                    smp = 0;
+                    depth = 0;
+                    col = mk(0.0f, 0.0f, 0.0f);
+                    TMPT_CAMERA_SAMPLE()
+                }
+                res += take;
+            }
+            // ---- finished queries: shade
+            if (has_pix && !in_query) {
+                bool finish = false;
+                f3 color = mk(0.0f, 0.0f, 0.0f);
+                if (!qany) {  // closest hit (Trace, main.cpp:91-109)
+                    if (ts.best >= 0) {  // Scatter, main.cpp:44-73
+                        f3 pos, nrm;
+                        hit_record(sv, ts.best, ts.bu, ts.bv, pos, nrm);
+                        light[depth * BLOCK] = light_cosine(nrm, r.d);  // zeroed if occluded
+                        f3 rnd = random_unit_vector(rng, sv.sincos);
+                        f3 target = pos + nrm + rnd;
+                        f3 nd = normalize(target - pos);
+                        nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
+                        nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
+                        ++depth;
+                        TMPT_START_QUERY(pos, ldir, true)
+                    } else {
+                        color = sky(r.d);  // main.cpp:106-107
+                        finish = true;
+                    }
+                } else {  // shadow query of bounce depth-1
+                    if (ts.best >= 0) light[(depth - 1) * BLOCK] = 0.0f;
+                    if (depth < (uint32_t)kMaxDepth) {
+                        TMPT_START_QUERY(mk(nxt[0], nxt[BLOCK], nxt[2 * BLOCK]),
+                                         mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]), false)
+                    } else {
+                        finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
+                    }
+                }
+                if (finish) {
+                    for (int kk = (int)depth - 1; kk >= 0; --kk)
+                        color = backward_step(color, light[kk * BLOCK]);
+                    col = col + color;
+                    ++smp;
+                    depth = 0;
+                    if (smp < (uint32_t)a.spp) {
+                        TMPT_CAMERA_SAMPLE()
+                    } else {
+                        out[pix] = pack_pixel(col, a.spp_recip);
+                        has_pix = false;
+                    }
+                }
+            }
+        }
+        if (!__any(in_query)) {
+            if (exhausted && !__any(has_pix)) break;
+            continue;
+        }
+        for (int k = 0; k < STEPS; ++k) {  // traversal rounds
+            const uint64_t at_leaf = __ballot(in_query && ts.node < 0);
+            const uint64_t at_node = __ballot(in_query && ts.node >= 0);
+            if ((at_leaf | at_node) == 0) break;
+            const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
+            // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds
+            // (latency of the few remaining pixels over lane efficiency)
+            const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
+            if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
+                if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, cnt)) in_query = false;
+            }
+        }
+    }
+#undef TMPT_CAMERA_SAMPLE
+#undef TMPT_START_QUERY
+    uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
+    uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
+    uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
+    if (lane_id() == 0) {
+        atomicAdd(&counters[0], (unsigned long long)(re + rs));
+        atomicAdd(&counters[3], (unsigned long long)re);
+        if (COUNT) {
+            atomicAdd(&counters[1], (unsigned long long)nv);
+            atomicAdd(&counters[2], (unsigned long long)nt);
+        }
+    }
+}
+
 // ============================================================ host side
 namespace {
 
@@ -768,6 +950,40 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     return 0;
 }
 
+// Persistent path engine: one launch per frame (shard).
+int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
+                      unsigned long long* d_counters)
+{
+    constexpr int kPathSL = 16, kPathSteps = 8, kShadeMin = 8;
+    auto fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin>
+                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin>;
+    // TMPT_TUNE=900,<steps>,<shade_min>,<vote>: tuning variants of the path kernel
+    if (const char* tune = getenv("TMPT_TUNE")) {
+        int a0 = 0, a1 = 0, a2 = 0, a3 = 1;
+        if (sscanf(tune, "%d,%d,%d,%d", &a0, &a1, &a2, &a3) == 4 && a0 == 900 && !count) {
+#define TMPT_PV(ST_, SM_, V_) \
+    if (a1 == ST_ && a2 == SM_ && a3 == V_) fn = k_path<false, kBlk, kPathSL, ST_, SM_, V_>;
+            TMPT_PV(2, 16, 1) TMPT_PV(8, 16, 1) TMPT_PV(16, 16, 1) TMPT_PV(4, 4, 1) TMPT_PV(4, 8, 1)
+            TMPT_PV(4, 32, 1) TMPT_PV(4, 16, 0) TMPT_PV(8, 8, 1) TMPT_PV(8, 32, 1) TMPT_PV(2, 8, 1)
+            TMPT_PV(8, 8, 2) TMPT_PV(4, 8, 2)
+#undef TMPT_PV
+        }
+    }
+    int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
+    const size_t head_words = (size_t)kSeg * kCtr;
+    if (ensure_ws(s, (ovf_words + head_words) * 4)) return -1;
+    uint32_t* heads = (uint32_t*)s.ws + ovf_words;
+    TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
+    PathCtl pc;
+    pc.heads = heads;
+    pc.P = a.slots;
+    pc.seg_cap = (uint32_t)std::max<int64_t>(1, (a.slots + kSeg - 1) / kSeg);
+    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, pc, d_out, (uint32_t*)s.ws, d_counters);
+    TMPT_HIP(hipGetLastError());
+    return 0;
+}
+
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
                     float* d_hits, int32_t* d_ids)
 {
@@ -805,12 +1021,14 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     TMPT_HIP(hipEventRecord(e0, s.stream));
     int rc = 0;
     bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode == TMPT_SEED_PIXEL;
+    bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_PIXEL && use_wide();
     s.extend_ms = s.shadow_ms = 0;
     s.extend_rays = s.shadow_rays = s.node_visits = s.tri_tests = 0;
     s.shadow_node_visits = s.shadow_tri_tests = 0;
     s.extend_launches = s.shadow_launches = s.iterations = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
+        else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
         else rc = render_megakernel(s, a, d_out, count, d_counters);
     }
     (void)hipEventRecord(e1, s.stream);
@@ -829,7 +1047,15 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         return -1;
     }
     s.render_ms = ms;
-    if (!wave) {
+    if (persistent) {  // one kernel for both query kinds
+        s.extend_ms = ms;
+        s.extend_rays = c[3];
+        s.shadow_rays = c[0] - c[3];
+        s.node_visits = c[1];
+        s.tri_tests = c[2];
+        s.extend_launches = 1;
+        s.iterations = 1;
+    } else if (!wave) {
         s.extend_ms = ms;
         s.extend_rays = c[0];
         s.node_visits = c[1];

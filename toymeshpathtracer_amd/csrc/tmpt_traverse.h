@@ -262,6 +262,82 @@ __device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r
     return false;
 }
 
+// Same step with the query kind chosen per lane at run time (the persistent
+// path engine mixes closest-hit and shadow queries in one wave): children are
+// always visited near to far; a shadow query stops at its first accepted hit.
+template <bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step4_mixed(const SceneView& sv, const TravRay& r, bool any,
+                                                 TravState& ts, TravStack<BLOCK, SL>& st,
+                                                 TravCount& cnt)
+{
+    if (ts.node >= 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
+        uint4 A = p[0], B = p[1], C = p[2];
+        int4 L = reinterpret_cast<const int4*>(p)[3];
+        if (COUNT) ++cnt.nodes;
+        const float ax = exp_scale(A.w) * r.ix, bx = (__uint_as_float(A.x) - r.o.x) * r.ix;
+        const float ay = exp_scale(A.w >> 8) * r.iy, by = (__uint_as_float(A.y) - r.o.y) * r.iy;
+        const float az = exp_scale(A.w >> 16) * r.iz, bz = (__uint_as_float(A.z) - r.o.z) * r.iz;
+        const uint32_t mask = A.w >> 24;
+        float key[4];
+        int ch[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sh = 8 * k;
+            float t0x = __builtin_fmaf((float)((B.x >> sh) & 255u), ax, bx);
+            float t1x = __builtin_fmaf((float)((B.y >> sh) & 255u), ax, bx);
+            float t0y = __builtin_fmaf((float)((B.z >> sh) & 255u), ay, by);
+            float t1y = __builtin_fmaf((float)((B.w >> sh) & 255u), ay, by);
+            float t0z = __builtin_fmaf((float)((C.x >> sh) & 255u), az, bz);
+            float t1z = __builtin_fmaf((float)((C.y >> sh) & 255u), az, bz);
+            float tn = max3f(fminf(t0x, t1x), fminf(t0y, t1y), fmaxf(fminf(t0z, t1z), 0.0f));
+            float tf = min3f(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fminf(fmaxf(t0z, t1z), ts.bt));
+            bool hit = ((mask >> k) & 1u) && tn <= tf * kTfarSlack;
+            key[k] = hit ? tn : INFINITY;
+        }
+        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
+                 (key[3] != INFINITY);
+        if (nh > 0) {
+#define TMPT_CSWAP(i, j)                                            \
+    if (key[j] < key[i]) {                                          \
+        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
+        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
+    }
+            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
+#undef TMPT_CSWAP
+            if (nh > 3) st.push(ts.sp, ch[3]);
+            if (nh > 2) st.push(ts.sp, ch[2]);
+            if (nh > 1) st.push(ts.sp, ch[1]);
+            ts.node = ch[0];
+            return false;
+        }
+    } else {
+        const uint32_t code = (uint32_t)ts.node;
+        const uint32_t first = code & kLeafFirstMask;
+        const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
+        for (uint32_t k = 0; k < n; ++k) {
+            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
+            float4 a = p[0], b = p[1], c = p[2];
+            if (COUNT) ++cnt.tris;
+            float t, u, v;
+            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
+                        t, u, v)) {
+                int id = __float_as_int(c.y);
+                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                    ts.bt = t;
+                    ts.bu = u;
+                    ts.bv = v;
+                    ts.best = id;
+                    if (any) return true;
+                }
+            }
+        }
+    }
+    if (ts.sp == 0) return true;
+    ts.node = st.pop(ts.sp);
+    return false;
+}
+
 template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
 __device__ __forceinline__ bool trav_step_w(const SceneView& sv, const TravRay& r, float tlo,
                                             float tmin, float tmax, TravState& ts,
