@@ -45,7 +45,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "MRays/s on sponza.obj 1920x1080 64spp at 1/2/4/8 GPUs; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 BAND_ROWS = 16
-S_NODE = 64            # bytes per visited BVH2 node in our layout (both child boxes + links)
+S_NODE = 64            # bytes per visited node: BVH4Q (4 quantised child boxes + links) or BVH2
 S_TRI = 36             # bytes per triangle test (3 x vec3), SURVEY.md §8d
 S_RAY = 32 + 16        # ray read + hit write, SURVEY.md §8d
 
@@ -67,6 +67,22 @@ def scene_path(obj: str) -> str:
         import gen_standin_sponza
         return gen_standin_sponza.ensure()
     return os.path.join(ROOT, "data", obj)
+
+
+def pmc_traffic() -> dict:
+    """HBM bytes per k_path launch from the newest committed PMC pass
+    (profiles/r*_pmc_k_path.json, written by tools/prof_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench; FETCH_SIZE x2 per
+    MI355X_MICROARCH.md).  PMC needs rocprofv3 around the process, so the live
+    bench cannot collect it itself; null when no profile is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_k_path.json")))
+    if not files:
+        return {"traffic": None}
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    return {"traffic": round(rec["hbm_bytes_per_launch"]), "traffic_unit": "bytes/launch",
+            "traffic_source": os.path.relpath(files[-1], ROOT), "traffic_kernel": rec["kernel"]}
 
 
 def main() -> None:
@@ -198,15 +214,16 @@ def main() -> None:
     elif engine == tm.ENGINE_PERSISTENT and cs.extend_rays and ext_launches:
         # one launch per frame serves both query kinds: per-query averages over all of them
         q = cs.extend_rays + cs.shadow_rays
-        n_node = cs.node_visits / q
-        n_tri = cs.tri_tests / q
+        n_node = (cs.node_visits + cs.shadow_node_visits) / q
+        n_tri = (cs.tri_tests + cs.shadow_tri_tests) / q
         b_ray = S_RAY + S_NODE * n_node + S_TRI * n_tri
         per_launch_rays = (ext_rays + sh_rays) / ext_launches
         avg_launch_ms = ext_ms / ext_launches
         achieved = b_ray * per_launch_rays / (avg_launch_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "kernel": "k_path (persistent: closest-hit + shadow queries + shading)",
+                **pmc_traffic(),
                 "bytes_per_ray": round(b_ray, 1), "n_node_per_ray": round(n_node, 2),
                 "n_tri_per_ray": round(n_tri, 2), "avg_launch_ms": round(avg_launch_ms, 4),
                 "rays_per_launch": round(per_launch_rays, 1)}

@@ -231,10 +231,17 @@ def test_device_output_pointer(gpu):
 def test_count_visits_instrumentation(gpu):
     tris, bmin, bmax, sc = _scene("suzanne.obj")
     cam = tm.Camera.for_scene(bmin, bmax, 160, 90)
-    img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, count_visits=True)
-    st = sc.stats()
-    assert st.extend_rays + st.shadow_rays == rays
-    assert st.node_visits > st.extend_rays and st.tri_tests > 0 and st.shadow_node_visits > 0
-    img2, _ = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL)
-    assert np.array_equal(img, img2)
+    seen = {}
+    for engine in (tm.ENGINE_WAVEFRONT, tm.ENGINE_PERSISTENT):
+        img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine,
+                                   count_visits=True)
+        st = sc.stats()
+        assert st.extend_rays + st.shadow_rays == rays
+        assert st.node_visits > st.extend_rays and st.tri_tests > 0 and st.shadow_node_visits > 0
+        img2, _ = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine)
+        assert np.array_equal(img, img2)
+        seen[engine] = (img, st.extend_rays, st.node_visits, st.tri_tests)
+    # closest-hit traversal is the same ordered walk in both engines: identical work
+    a, b = seen[tm.ENGINE_WAVEFRONT], seen[tm.ENGINE_PERSISTENT]
+    assert np.array_equal(a[0], b[0]) and a[1:] == b[1:]
     sc.close()

@@ -531,7 +531,7 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     float* light = &s_light[threadIdx.x];
     float* nxt = &s_next[threadIdx.x];
-    TravCount cnt;
+    TravCount cnt, cnt_s;  // COUNT: closest-hit and shadow queries apart
     uint32_t rays_e = 0, rays_s = 0;
     const f3 ldir = light_dir();
     const uint64_t lt = (1ull << lane_id()) - 1ull;
@@ -661,7 +661,15 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
             // (latency of the few remaining pixels over lane efficiency)
             const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
             if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
-                if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, cnt)) in_query = false;
+                if (COUNT) {
+                    TravCount c1;
+                    if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, c1)) in_query = false;
+                    TravCount& dst = qany ? cnt_s : cnt;
+                    dst.nodes += c1.nodes;
+                    dst.tris += c1.tris;
+                } else if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, cnt)) {
+                    in_query = false;
+                }
             }
         }
     }
@@ -670,12 +678,16 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
     uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
     uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
     uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
+    uint32_t nvs = COUNT ? wave_sum(cnt_s.nodes) : 0u;
+    uint32_t nts = COUNT ? wave_sum(cnt_s.tris) : 0u;
     if (lane_id() == 0) {
         atomicAdd(&counters[0], (unsigned long long)(re + rs));
         atomicAdd(&counters[3], (unsigned long long)re);
         if (COUNT) {
             atomicAdd(&counters[1], (unsigned long long)nv);
             atomicAdd(&counters[2], (unsigned long long)nt);
+            atomicAdd(&counters[4], (unsigned long long)nvs);
+            atomicAdd(&counters[5], (unsigned long long)nts);
         }
     }
 }
@@ -1013,8 +1025,8 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     RenderArgs a = make_args(cam, d);
     bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
     unsigned long long* d_counters = nullptr;
-    TMPT_HIP(hipMallocAsync((void**)&d_counters, 4 * sizeof(unsigned long long), s.stream));
-    TMPT_HIP(hipMemsetAsync(d_counters, 0, 4 * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipMallocAsync((void**)&d_counters, 6 * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipMemsetAsync(d_counters, 0, 6 * sizeof(unsigned long long), s.stream));
     hipEvent_t e0, e1;
     TMPT_HIP(hipEventCreate(&e0));
     TMPT_HIP(hipEventCreate(&e1));
@@ -1033,7 +1045,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     }
     (void)hipEventRecord(e1, s.stream);
     hipError_t se = hipStreamSynchronize(s.stream);
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
     if (rc == 0 && se == hipSuccess)
         se = hipMemcpy(c, d_counters, sizeof(c), hipMemcpyDeviceToHost);
     float ms = 0;
@@ -1053,6 +1065,8 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.shadow_rays = c[0] - c[3];
         s.node_visits = c[1];
         s.tri_tests = c[2];
+        s.shadow_node_visits = c[4];
+        s.shadow_tri_tests = c[5];
         s.extend_launches = 1;
         s.iterations = 1;
     } else if (!wave) {
