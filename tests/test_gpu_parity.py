@@ -6,6 +6,8 @@ here is exact, and Scene::HitScene results are compared bit for bit.
 """
 import hashlib
 
+import os
+
 import numpy as np
 import pytest
 
@@ -232,16 +234,23 @@ def test_count_visits_instrumentation(gpu):
     tris, bmin, bmax, sc = _scene("suzanne.obj")
     cam = tm.Camera.for_scene(bmin, bmax, 160, 90)
     seen = {}
-    for engine in (tm.ENGINE_WAVEFRONT, tm.ENGINE_PERSISTENT):
-        img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine,
-                                   count_visits=True)
-        st = sc.stats()
+    for engine, node in ((tm.ENGINE_WAVEFRONT, "q"), (tm.ENGINE_PERSISTENT, "q"), (tm.ENGINE_PERSISTENT, "f")):
+        os.environ["TMPT_NODE"] = node
+        try:
+            img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine,
+                                       count_visits=True)
+            st = sc.stats()
+            img2, _ = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine)
+        finally:
+            del os.environ["TMPT_NODE"]
         assert st.extend_rays + st.shadow_rays == rays
         assert st.node_visits > st.extend_rays and st.tri_tests > 0 and st.shadow_node_visits > 0
-        img2, _ = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine)
         assert np.array_equal(img, img2)
-        seen[engine] = (img, st.extend_rays, st.node_visits, st.tri_tests)
-    # closest-hit traversal is the same ordered walk in both engines: identical work
-    a, b = seen[tm.ENGINE_WAVEFRONT], seen[tm.ENGINE_PERSISTENT]
+        seen[(engine, node)] = (img, st.extend_rays, st.node_visits, st.tri_tests)
+    # closest-hit traversal over BVH4Q is the same ordered walk in both engines: identical work
+    a, b = seen[(tm.ENGINE_WAVEFRONT, "q")], seen[(tm.ENGINE_PERSISTENT, "q")]
     assert np.array_equal(a[0], b[0]) and a[1:] == b[1:]
+    # BVH4F (unquantised boxes) culls at least as tightly, same image
+    c = seen[(tm.ENGINE_PERSISTENT, "f")]
+    assert np.array_equal(a[0], c[0]) and c[1] == a[1] and c[2] <= a[2] and c[3] <= a[3]
     sc.close()

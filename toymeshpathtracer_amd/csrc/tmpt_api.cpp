@@ -153,6 +153,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.nodes) (void)hipFree(s.nodes);
     if (s.nodes4) (void)hipFree(s.nodes4);
+    if (s.nodes4f) (void)hipFree(s.nodes4f);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);

@@ -465,7 +465,9 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
                                                        const int2* __restrict__ frontier, int nf,
                                                        int2* __restrict__ next,
                                                        uint32_t* __restrict__ counters,
-                                                       Bvh4Node* __restrict__ out, int leaf_max)
+                                                       Bvh4Node* __restrict__ out,
+                                                       Bvh4FNode* __restrict__ outf, int leaf_max,
+                                                       int n_tris)
 {
     int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= nf) return;
@@ -517,8 +519,13 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
         scale[a] = ldexp(1.0, e);
         ebits |= (uint32_t)(e + 127) << (8 * a);
     }
-    int4 links = make_int4(0, 0, 0, 0);
+    // empty slots: inverted quantised box (lo 255 > hi 0) and a link to the null
+    // leaf, so a step that does not consult the mask still finds nothing there
+    const int null_leaf = (int)(0x80000000u | (uint32_t)n_tris);
+    int4 links = make_int4(null_leaf, null_leaf, null_leaf, null_leaf);
     int* lk = &links.x;
+    for (int k = nc; k < 4; ++k)
+        for (int a = 0; a < 3; ++a) qlo[a] |= 255u << (8 * k);
     for (int k = 0; k < nc; ++k) {
         for (int a = 0; a < 3; ++a) {
             double l = floor(((double)bx[k][a] - (double)lo[a]) / scale[a]);
@@ -541,6 +548,17 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
             next[qi] = make_int2(c, (int)slot);
             lk[k] = (int)slot;
         }
+    }
+    {
+        float pl[6][4];
+        for (int k = 0; k < 4; ++k)
+            for (int a = 0; a < 3; ++a) {
+                pl[2 * a][k] = k < nc ? bx[k][a] : INFINITY;
+                pl[2 * a + 1][k] = k < nc ? bx[k][3 + a] : -INFINITY;
+            }
+        for (int j = 0; j < 6; ++j) outf[dst].p[j] = f4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
+        outf[dst].links = links;
+        outf[dst].pad = make_int4(0, 0, 0, 0);
     }
     out[dst].a = f4(lo[0], lo[1], lo[2], __uint_as_float(ebits | (mask << 24)));
     out[dst].b = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
@@ -585,7 +603,11 @@ int build_lbvh(Scene& s, const float* d_tris9)
     s.n_nodes = m;
     TMPT_HIP(hipMalloc(&s.nodes, sizeof(BvhNode) * (size_t)m));
     TMPT_HIP(hipMalloc(&s.nodes4, sizeof(Bvh4Node) * (size_t)m));
-    TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * (size_t)std::max(n, 1)));
+    TMPT_HIP(hipMalloc(&s.nodes4f, sizeof(Bvh4FNode) * (size_t)m));
+    // one extra slot: the null triangle (all zero: det = 0, never accepted) that
+    // empty BVH4 child slots link to
+    TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * ((size_t)n + 1)));
+    TMPT_HIP(hipMemsetAsync(s.tri_pre + n, 0, sizeof(TriPre), st));
     TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(n, 1)));
     if (n == 0) {
         TMPT_HIP(hipMemsetAsync(s.nodes, 0, sizeof(BvhNode), st));
@@ -754,7 +776,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
         int2 *fa = fr0, *fb = fr1;
         while (nf > 0) {
             k_bvh4_level<<<blocks_for(nf, kBlock), kBlock, 0, st>>>(tchild, trange, leaf, tvals, tib, fa, nf,
-                                                                    fb, c4, s.nodes4, leaf_max);
+                                                                    fb, c4, s.nodes4, s.nodes4f, leaf_max, n);
             ++levels;
             if (hipMemcpyAsync(hc, c4, sizeof(hc), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }

@@ -45,6 +45,17 @@ struct alignas(16) Bvh4Node {
     int4 d;
 };
 static_assert(sizeof(Bvh4Node) == 64, "BVH4Q node is one half cache line");
+
+// BVH4F: the same 4-wide tree with full-precision child boxes, one 128-B line
+// per node.  Planes are grouped [axis][lo|hi][child] so a ray picks its near and
+// far plane of an axis by a byte offset (octant), not by per-child min/max; an
+// empty child slot has lo = +inf, hi = -inf and misses every ray.
+struct alignas(128) Bvh4FNode {
+    float4 p[6];  // lo_x, hi_x, lo_y, hi_y, lo_z, hi_z (child k in component k)
+    int4 links;
+    int4 pad;
+};
+static_assert(sizeof(Bvh4FNode) == 128, "BVH4F node is one 128-B line");
 constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
@@ -80,6 +91,7 @@ struct Scene {
     int32_t max_depth = 0;  // of the LBVH
     BvhNode* nodes = nullptr;
     Bvh4Node* nodes4 = nullptr;
+    Bvh4FNode* nodes4f = nullptr;  // same tree, f32 child boxes
     int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
     bool has_bvh2 = true;  // the LBVH2 (A/B layout) matches tri_pre only for the LBVH builder
     TriPre* tri_pre = nullptr;

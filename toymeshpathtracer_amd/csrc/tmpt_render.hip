@@ -516,10 +516,12 @@ struct PathCtl {
     uint32_t* heads;  // kSeg pixel-segment heads, stride kCtr
     uint32_t seg_cap;
     int64_t P;
+    int cost_map;  // COUNT only: write per-pixel traversal work instead of colour
 };
 
-template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1>
-__global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, PathCtl pc,
+template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
+          int OCC = 1>
+__global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
                                                 unsigned long long* __restrict__ counters)
@@ -540,6 +542,10 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
     bool exhausted = pc.P == 0;
     bool has_pix = false, in_query = false, qany = false;
     uint32_t pix = 0, rng = 0, smp = 0, depth = 0;
+    uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
+    // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
+    // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
+    uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
     f3 col = mk(0.0f, 0.0f, 0.0f);
     TravRay r;
     TravState ts;
@@ -569,6 +575,11 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
         const uint64_t need = __ballot(wants);
         const uint64_t trav = __ballot(in_query);
         if (need != 0 && (__popcll(need) >= SHADE_MIN || trav == 0)) {
+            if (COUNT) {
+                ++rs_sr;
+                rs_sl += (uint64_t)__popcll(need);
+                rs_st += (uint64_t)__popcll(trav);
+            }
             // ---- new pixels for idle lanes (wave-uniform reservation)
             const uint64_t nopix = __ballot(!has_pix && !exhausted);
             if (nopix != 0) {
@@ -600,6 +611,7 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
                     smp = 0;
                     depth = 0;
                     col = mk(0.0f, 0.0f, 0.0f);
+                    if (COUNT) work0 = cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
                     TMPT_CAMERA_SAMPLE()
                 }
                 res += take;
@@ -642,7 +654,9 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
                     if (smp < (uint32_t)a.spp) {
                         TMPT_CAMERA_SAMPLE()
                     } else {
-                        out[pix] = pack_pixel(col, a.spp_recip);
+                        out[pix] = (COUNT && pc.cost_map)
+                                       ? cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris - work0
+                                       : pack_pixel(col, a.spp_recip);
                         has_pix = false;
                     }
                 }
@@ -660,14 +674,18 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
             // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds
             // (latency of the few remaining pixels over lane efficiency)
             const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
+            if (COUNT) {
+                if (!vote || !leaf_round) { ++rs_nr; rs_nl += (uint64_t)__popcll(at_node); }
+                if (!vote || leaf_round) { ++rs_lr; rs_ll += (uint64_t)__popcll(at_leaf); }
+            }
             if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
                 if (COUNT) {
                     TravCount c1;
-                    if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, c1)) in_query = false;
+                    if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, c1)) in_query = false;
                     TravCount& dst = qany ? cnt_s : cnt;
                     dst.nodes += c1.nodes;
                     dst.tris += c1.tris;
-                } else if (trav_step4_mixed<COUNT>(sv, r, qany, ts, st, cnt)) {
+                } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
                     in_query = false;
                 }
             }
@@ -688,6 +706,13 @@ __global__ void __launch_bounds__(BLOCK) k_path(SceneView sv, RenderArgs a, Path
             atomicAdd(&counters[2], (unsigned long long)nt);
             atomicAdd(&counters[4], (unsigned long long)nvs);
             atomicAdd(&counters[5], (unsigned long long)nts);
+            atomicAdd(&counters[6], (unsigned long long)rs_nr);
+            atomicAdd(&counters[7], (unsigned long long)rs_nl);
+            atomicAdd(&counters[8], (unsigned long long)rs_lr);
+            atomicAdd(&counters[9], (unsigned long long)rs_ll);
+            atomicAdd(&counters[10], (unsigned long long)rs_sr);
+            atomicAdd(&counters[11], (unsigned long long)rs_sl);
+            atomicAdd(&counters[12], (unsigned long long)rs_st);
         }
     }
 }
@@ -723,7 +748,8 @@ int ensure_ws(Scene& s, size_t bytes)
 
 SceneView view(const Scene& s)
 {
-    return SceneView{s.nodes, s.nodes4, s.tri_pre, s.tri_orig, s.sincos, s.n};
+    return SceneView{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
+                     s.tri_orig, s.sincos, s.n};
 }
 
 RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
@@ -967,17 +993,27 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                       unsigned long long* d_counters)
 {
     constexpr int kPathSL = 16, kPathSteps = 8, kShadeMin = 8;
-    auto fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin>
-                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin>;
+    // node format (TMPT_NODE, A/B): q = BVH4Q min/max decode, f = BVH4F f32 boxes,
+    // default = BVH4Q octant decode
+    const char* nf = getenv("TMPT_NODE");
+    const int fmt = nf && nf[0] == 'q' ? 0 : (nf && nf[0] == 'f' ? 1 : 2);
+    using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
+    PathFn fn = nullptr;
+#define TMPT_PF(C_, F_) \
+    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_>;
+    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2)
+#undef TMPT_PF
+    const bool quant = fmt == 0;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
-        int a0 = 0, a1 = 0, a2 = 0, a3 = 1;
-        if (sscanf(tune, "%d,%d,%d,%d", &a0, &a1, &a2, &a3) == 4 && a0 == 900 && !count) {
-#define TMPT_PV(ST_, SM_, V_) \
-    if (a1 == ST_ && a2 == SM_ && a3 == V_) fn = k_path<false, kBlk, kPathSL, ST_, SM_, V_>;
-            TMPT_PV(2, 16, 1) TMPT_PV(8, 16, 1) TMPT_PV(16, 16, 1) TMPT_PV(4, 4, 1) TMPT_PV(4, 8, 1)
-            TMPT_PV(4, 32, 1) TMPT_PV(4, 16, 0) TMPT_PV(8, 8, 1) TMPT_PV(8, 32, 1) TMPT_PV(2, 8, 1)
-            TMPT_PV(8, 8, 2) TMPT_PV(4, 8, 2)
+        int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 1;
+        if (sscanf(tune, "%d,%d,%d,%d,%d", &a0, &a1, &a2, &a3, &a4) >= 4 && a0 == 900 && !count) {
+#define TMPT_PV(ST_, SM_, V_, O_)                                                  \
+    if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == O_)                           \
+        fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, O_>               \
+                   : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, O_>     \
+                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 2, O_>);
+            TMPT_PV(4, 8, 1, 1) TMPT_PV(16, 16, 1, 1) TMPT_PV(8, 8, 1, 5)
 #undef TMPT_PV
         }
     }
@@ -988,6 +1024,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     uint32_t* heads = (uint32_t*)s.ws + ovf_words;
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
     PathCtl pc;
+    // TMPT_COST_MAP=1 (diagnostic, instrumented renders only): the output
+    // receives each pixel's traversal work (node visits + triangle tests)
+    const char* cm = getenv("TMPT_COST_MAP");
+    pc.cost_map = count && cm && atoi(cm) != 0;
     pc.heads = heads;
     pc.P = a.slots;
     pc.seg_cap = (uint32_t)std::max<int64_t>(1, (a.slots + kSeg - 1) / kSeg);
@@ -1025,8 +1065,9 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     RenderArgs a = make_args(cam, d);
     bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
     unsigned long long* d_counters = nullptr;
-    TMPT_HIP(hipMallocAsync((void**)&d_counters, 6 * sizeof(unsigned long long), s.stream));
-    TMPT_HIP(hipMemsetAsync(d_counters, 0, 6 * sizeof(unsigned long long), s.stream));
+    constexpr int kCounters = 16;
+    TMPT_HIP(hipMallocAsync((void**)&d_counters, kCounters * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipMemsetAsync(d_counters, 0, kCounters * sizeof(unsigned long long), s.stream));
     hipEvent_t e0, e1;
     TMPT_HIP(hipEventCreate(&e0));
     TMPT_HIP(hipEventCreate(&e1));
@@ -1045,7 +1086,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     }
     (void)hipEventRecord(e1, s.stream);
     hipError_t se = hipStreamSynchronize(s.stream);
-    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long c[kCounters] = {};
     if (rc == 0 && se == hipSuccess)
         se = hipMemcpy(c, d_counters, sizeof(c), hipMemcpyDeviceToHost);
     float ms = 0;
@@ -1069,6 +1110,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.shadow_tri_tests = c[5];
         s.extend_launches = 1;
         s.iterations = 1;
+        if (count && getenv("TMPT_ROUND_LOG"))  // diagnostic: wave-round efficiency
+            fprintf(stderr,
+                    "k_path rounds: node %llu (%.1f lanes), leaf %llu (%.1f lanes), shade %llu "
+                    "(%.1f wanting, %.1f traversing)\n",
+                    c[6], c[6] ? (double)c[7] / c[6] : 0.0, c[8], c[8] ? (double)c[9] / c[8] : 0.0,
+                    c[10], c[10] ? (double)c[11] / c[10] : 0.0, c[10] ? (double)c[12] / c[10] : 0.0);
     } else if (!wave) {
         s.extend_ms = ms;
         s.extend_rays = c[0];

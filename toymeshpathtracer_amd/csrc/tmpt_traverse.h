@@ -28,6 +28,7 @@ struct TravRay {
     f3 o, d;
     float ix, iy, iz;  // 1/d (finite)
     float ox, oy, oz;  // o * inv
+    uint32_t offx, offy, offz;  // BVH4F byte offset of the near plane per axis (far = ^16)
 };
 
 __device__ __forceinline__ TravRay make_trav_ray(f3 o, f3 d)
@@ -41,6 +42,10 @@ __device__ __forceinline__ TravRay make_trav_ray(f3 o, f3 d)
     r.ox = o.x * r.ix;
     r.oy = o.y * r.iy;
     r.oz = o.z * r.iz;
+    // 1/d > 0: the lo plane is entered first; < 0: the hi plane (never 0: safe_inv)
+    r.offx = signbit(r.ix) ? 16u : 0u;
+    r.offy = signbit(r.iy) ? 48u : 32u;
+    r.offz = signbit(r.iz) ? 80u : 64u;
     return r;
 }
 
@@ -60,10 +65,19 @@ __device__ __forceinline__ bool slab(const TravRay& r, float lx, float ly, float
     return tn <= tf * kTfarSlack;
 }
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// Per-lane traversal stack: the top SL entries in LDS ([depth][lane], a wave's
+// access to one depth hits 64 banks), deeper ones in a per-lane global area.
+// The LDS pointer is address-space-3 typed so the compiler emits ds_read /
+// ds_write; a generic pointer let it merge the two pop paths into one FLAT
+// load, which goes through the vector-memory address unit (TA) like a global
+// load -- one extra TA slot per traversal step.
 template <int BLOCK, int SL>
 struct TravStack {
-    uint32_t* lds;   // &s_stack[threadIdx.x]; entry k at lds[k * BLOCK]
+    lds_u32* lds;    // &s_stack[threadIdx.x]; entry k at lds[k * BLOCK]
     uint32_t* glob;  // kStackTotal - SL entries of this lane
+    __device__ __forceinline__ TravStack(uint32_t* l, uint32_t* g) : lds((lds_u32*)l), glob(g) {}
     __device__ __forceinline__ void push(int& sp, int v)
     {
         if (SL >= kStackTotal || sp < SL) lds[sp * BLOCK] = (uint32_t)v;
@@ -73,14 +87,17 @@ struct TravStack {
     __device__ __forceinline__ int pop(int& sp)
     {
         --sp;
-        if (SL >= kStackTotal || sp < SL) return (int)lds[sp * BLOCK];
-        return (int)glob[sp - SL];
+        if (SL >= kStackTotal) return (int)lds[sp * BLOCK];
+        uint32_t v = lds[min(sp, SL - 1) * BLOCK];
+        if (sp >= SL) v = glob[sp - SL];
+        return (int)v;
     }
 };
 
 struct SceneView {
     const BvhNode* __restrict__ nodes;
     const Bvh4Node* __restrict__ nodes4;
+    const char* __restrict__ nodes4f;  // Bvh4FNode array, addressed by byte offset
     const TriPre* __restrict__ tri_pre;
     const TriOrig* __restrict__ tri_orig;
     const float2* __restrict__ sincos;
@@ -336,6 +353,205 @@ __device__ __forceinline__ bool trav_step4_mixed(const SceneView& sv, const Trav
     if (ts.sp == 0) return true;
     ts.node = st.pop(ts.sp);
     return false;
+}
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// One step over BVH4F (f32 child boxes): near/far planes chosen by the ray's
+// octant (byte offsets), slab distances by packed fma over child pairs, so a
+// node costs 12 v_pk_fma + 4 compares per child instead of per-child unpacking
+// and min/max.  The same children, links, order and leaf handling as
+// trav_step4_mixed; boxes are the unquantised padded boxes (tighter).
+template <bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step4f_mixed(const SceneView& sv, const TravRay& r, bool any,
+                                                  TravState& ts, TravStack<BLOCK, SL>& st,
+                                                  TravCount& cnt)
+{
+    if (ts.node >= 0) {
+        const uint32_t nb = (uint32_t)ts.node << 7;
+        const char* base = sv.nodes4f;
+        const float4 nx = *reinterpret_cast<const float4*>(base + (nb | r.offx));
+        const float4 fx = *reinterpret_cast<const float4*>(base + (nb | (r.offx ^ 16u)));
+        const float4 ny = *reinterpret_cast<const float4*>(base + (nb | r.offy));
+        const float4 fy = *reinterpret_cast<const float4*>(base + (nb | (r.offy ^ 16u)));
+        const float4 nz = *reinterpret_cast<const float4*>(base + (nb | r.offz));
+        const float4 fz = *reinterpret_cast<const float4*>(base + (nb | (r.offz ^ 16u)));
+        const int4 L = *reinterpret_cast<const int4*>(base + (nb | 96u));
+        if (COUNT) ++cnt.nodes;
+        const v2f ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+        const v2f ox = {-r.ox, -r.ox}, oy = {-r.oy, -r.oy}, oz = {-r.oz, -r.oz};
+#define TMPT_PL(V, I, O, lo2, hi2)                                                   \
+        const v2f lo2 = __builtin_elementwise_fma((v2f){V.x, V.y}, I, O);               \
+        const v2f hi2 = __builtin_elementwise_fma((v2f){V.z, V.w}, I, O);
+        TMPT_PL(nx, ix, ox, nx01, nx23)
+        TMPT_PL(fx, ix, ox, fx01, fx23)
+        TMPT_PL(ny, iy, oy, ny01, ny23)
+        TMPT_PL(fy, iy, oy, fy01, fy23)
+        TMPT_PL(nz, iz, oz, nz01, nz23)
+        TMPT_PL(fz, iz, oz, fz01, fz23)
+#undef TMPT_PL
+        const float tnear[4] = {nx01.x, nx01.y, nx23.x, nx23.y};
+        const float tnear_y[4] = {ny01.x, ny01.y, ny23.x, ny23.y};
+        const float tnear_z[4] = {nz01.x, nz01.y, nz23.x, nz23.y};
+        const float tfar[4] = {fx01.x, fx01.y, fx23.x, fx23.y};
+        const float tfar_y[4] = {fy01.x, fy01.y, fy23.x, fy23.y};
+        const float tfar_z[4] = {fz01.x, fz01.y, fz23.x, fz23.y};
+        float key[4];
+        int ch[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float tn = fmaxf(fmaxf(tnear[k], tnear_y[k]), fmaxf(tnear_z[k], 0.0f));
+            float tf = fminf(fminf(tfar[k], tfar_y[k]), fminf(tfar_z[k], ts.bt));
+            key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
+        }
+        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
+                 (key[3] != INFINITY);
+        if (nh > 0) {
+#define TMPT_CSWAP(i, j)                                            \
+    if (key[j] < key[i]) {                                          \
+        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
+        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
+    }
+            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
+#undef TMPT_CSWAP
+            if (nh > 3) st.push(ts.sp, ch[3]);
+            if (nh > 2) st.push(ts.sp, ch[2]);
+            if (nh > 1) st.push(ts.sp, ch[1]);
+            ts.node = ch[0];
+            return false;
+        }
+    } else {
+        const uint32_t code = (uint32_t)ts.node;
+        const uint32_t first = code & kLeafFirstMask;
+        const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
+        for (uint32_t k = 0; k < n; ++k) {
+            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
+            float4 a = p[0], b = p[1], c = p[2];
+            if (COUNT) ++cnt.tris;
+            float t, u, v;
+            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
+                        t, u, v)) {
+                int id = __float_as_int(c.y);
+                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                    ts.bt = t;
+                    ts.bu = u;
+                    ts.bv = v;
+                    ts.best = id;
+                    if (any) return true;
+                }
+            }
+        }
+    }
+    if (ts.sp == 0) return true;
+    ts.node = st.pop(ts.sp);
+    return false;
+}
+
+// One step over BVH4Q (64-B quantised nodes) with the BVH4F step's decoding:
+// near/far byte planes picked per axis by the ray's octant (one v_cndmask per
+// plane dword), t = q * (2^e/d) + fma(origin, 1/d, -o/d) by packed fma over
+// child pairs, no per-child min/max and no mask test (empty slots carry an
+// inverted box and link to the null leaf).  4 loads per node (the TA cost of a
+// divergent gather scales with bytes per lane) at ~BVH4F's VALU count.
+template <bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
+                                                   TravState& ts, TravStack<BLOCK, SL>& st,
+                                                   TravCount& cnt)
+{
+    if (ts.node >= 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
+        const uint4 A = p[0], B = p[1], C = p[2];
+        const int4 L = reinterpret_cast<const int4*>(p)[3];
+        if (COUNT) ++cnt.nodes;
+        const float sx = exp_scale(A.w) * r.ix, sy = exp_scale(A.w >> 8) * r.iy,
+                    sz = exp_scale(A.w >> 16) * r.iz;
+        const float bx = __builtin_fmaf(__uint_as_float(A.x), r.ix, -r.ox);
+        const float by = __builtin_fmaf(__uint_as_float(A.y), r.iy, -r.oy);
+        const float bz = __builtin_fmaf(__uint_as_float(A.z), r.iz, -r.oz);
+        const bool ngx = r.offx != 0u, ngy = r.offy != 32u, ngz = r.offz != 64u;
+        const uint32_t qnx = ngx ? B.y : B.x, qfx = ngx ? B.x : B.y;
+        const uint32_t qny = ngy ? B.w : B.z, qfy = ngy ? B.z : B.w;
+        const uint32_t qnz = ngz ? C.y : C.x, qfz = ngz ? C.x : C.y;
+        const v2f s2x = {sx, sx}, s2y = {sy, sy}, s2z = {sz, sz};
+        const v2f b2x = {bx, bx}, b2y = {by, by}, b2z = {bz, bz};
+#define TMPT_QB(Q, k) (float)(((Q) >> (8 * (k))) & 255u)
+#define TMPT_QP(Q, S, Bv, lo2, hi2)                                                              \
+        const v2f lo2 = __builtin_elementwise_fma((v2f){TMPT_QB(Q, 0), TMPT_QB(Q, 1)}, S, Bv);     \
+        const v2f hi2 = __builtin_elementwise_fma((v2f){TMPT_QB(Q, 2), TMPT_QB(Q, 3)}, S, Bv);
+        TMPT_QP(qnx, s2x, b2x, nx01, nx23)
+        TMPT_QP(qfx, s2x, b2x, fx01, fx23)
+        TMPT_QP(qny, s2y, b2y, ny01, ny23)
+        TMPT_QP(qfy, s2y, b2y, fy01, fy23)
+        TMPT_QP(qnz, s2z, b2z, nz01, nz23)
+        TMPT_QP(qfz, s2z, b2z, fz01, fz23)
+#undef TMPT_QP
+#undef TMPT_QB
+        const float tnx[4] = {nx01.x, nx01.y, nx23.x, nx23.y};
+        const float tny[4] = {ny01.x, ny01.y, ny23.x, ny23.y};
+        const float tnz[4] = {nz01.x, nz01.y, nz23.x, nz23.y};
+        const float tfx[4] = {fx01.x, fx01.y, fx23.x, fx23.y};
+        const float tfy[4] = {fy01.x, fy01.y, fy23.x, fy23.y};
+        const float tfz[4] = {fz01.x, fz01.y, fz23.x, fz23.y};
+        float key[4];
+        int ch[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float tn = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], 0.0f));
+            float tf = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], ts.bt));
+            key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
+        }
+        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
+                 (key[3] != INFINITY);
+        if (nh > 0) {
+#define TMPT_CSWAP(i, j)                                            \
+    if (key[j] < key[i]) {                                          \
+        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
+        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
+    }
+            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
+#undef TMPT_CSWAP
+            if (nh > 3) st.push(ts.sp, ch[3]);
+            if (nh > 2) st.push(ts.sp, ch[2]);
+            if (nh > 1) st.push(ts.sp, ch[1]);
+            ts.node = ch[0];
+            return false;
+        }
+    } else {
+        const uint32_t code = (uint32_t)ts.node;
+        const uint32_t first = code & kLeafFirstMask;
+        const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
+        for (uint32_t k = 0; k < n; ++k) {
+            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
+            float4 a = p[0], b = p[1], c = p[2];
+            if (COUNT) ++cnt.tris;
+            float t, u, v;
+            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
+                        t, u, v)) {
+                int id = __float_as_int(c.y);
+                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                    ts.bt = t;
+                    ts.bu = u;
+                    ts.bv = v;
+                    ts.best = id;
+                    if (any) return true;
+                }
+            }
+        }
+    }
+    if (ts.sp == 0) return true;
+    ts.node = st.pop(ts.sp);
+    return false;
+}
+
+// node format of the persistent engine: 0 = BVH4Q (mask + min/max decode),
+// 1 = BVH4F (f32 boxes), 2 = BVH4Q with octant decode
+template <int FMT, bool COUNT, int BLOCK, int SL>
+__device__ __forceinline__ bool trav_step_fmt(const SceneView& sv, const TravRay& r, bool any,
+                                              TravState& ts, TravStack<BLOCK, SL>& st, TravCount& cnt)
+{
+    if (FMT == 1) return trav_step4f_mixed<COUNT>(sv, r, any, ts, st, cnt);
+    if (FMT == 2) return trav_step4q2_mixed<COUNT>(sv, r, any, ts, st, cnt);
+    return trav_step4_mixed<COUNT>(sv, r, any, ts, st, cnt);
 }
 
 template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
