@@ -520,7 +520,7 @@ struct PathCtl {
 };
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
-          int OCC = 1>
+          int OCC = 1, int TAIL = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -551,35 +551,30 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     TravState ts;
     trav_init(ts, kMaxT);
 
-#define TMPT_START_QUERY(O_, D_, ANY_)                                         \
-    {                                                                          \
-        const f3 qo_ = (O_), qd_ = (D_);                                       \
-        r = make_trav_ray(qo_, qd_);                                           \
-        trav_init(ts, kMaxT);                                                  \
-        qany = (ANY_);                                                         \
-        if (qany) ++rays_s; else ++rays_e;                                     \
-        in_query = !ray_has_nan(qo_, qd_); /* NaN: a counted miss */           \
-    }
-#define TMPT_CAMERA_SAMPLE()                                                   \
-    {                                                                          \
-        const int lr_ = (int)(pix / (uint32_t)a.W);                            \
-        const int x_ = (int)(pix - (uint32_t)lr_ * (uint32_t)a.W);             \
-        f3 co_, cd_;                                                           \
-        camera_sample(a.cam, (uint32_t)x_, (uint32_t)tile_row_to_y(a, lr_),     \
-                      a.invW, a.invH, rng, co_, cd_);                          \
-        TMPT_START_QUERY(co_, cd_, false)                                      \
-    }
-
     for (;;) {
         const bool wants = has_pix ? !in_query : !exhausted;
         const uint64_t need = __ballot(wants);
         const uint64_t trav = __ballot(in_query);
-        if (need != 0 && (__popcll(need) >= SHADE_MIN || trav == 0)) {
+        // Sparse waves (TAIL = D > 0): a wave shades once SHADE_MIN lanes wait, or
+        // -- when fewer than D*SHADE_MIN lanes still hold a pixel -- once 1/D of
+        // them wait, so the last pixels of a wave (the frame's critical path at
+        // low load) do not idle until every other lane's query has finished.
+        int shade_min = SHADE_MIN;
+        if (TAIL > 0) {
+            const int act = __popcll(__ballot(has_pix));
+            shade_min = max(1, min(SHADE_MIN, act / TAIL));
+        }
+        if (need != 0 && (__popcll(need) >= shade_min || trav == 0)) {
             if (COUNT) {
                 ++rs_sr;
                 rs_sl += (uint64_t)__popcll(need);
                 rs_st += (uint64_t)__popcll(trav);
             }
+            // Each lane decides at most one next query this round; camera
+            // sampling and the query set-up are emitted once, after the
+            // branches, so the wave runs each at most once per round.
+            bool cam = false, start = false, sany = false;
+            f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
             // ---- new pixels for idle lanes (wave-uniform reservation)
             const uint64_t nopix = __ballot(!has_pix && !exhausted);
             if (nopix != 0) {
@@ -612,12 +607,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     depth = 0;
                     col = mk(0.0f, 0.0f, 0.0f);
                     if (COUNT) work0 = cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
-                    TMPT_CAMERA_SAMPLE()
+                    cam = true;
                 }
                 res += take;
             }
             // ---- finished queries: shade
-            if (has_pix && !in_query) {
+            if (has_pix && !in_query && !cam) {
                 bool finish = false;
                 f3 color = mk(0.0f, 0.0f, 0.0f);
                 if (!qany) {  // closest hit (Trace, main.cpp:91-109)
@@ -631,7 +626,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
                         nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
                         ++depth;
-                        TMPT_START_QUERY(pos, ldir, true)
+                        start = true;  // shadow query toward the light
+                        sany = true;
+                        so = pos;
+                        sd = ldir;
                     } else {
                         color = sky(r.d);  // main.cpp:106-107
                         finish = true;
@@ -639,8 +637,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 } else {  // shadow query of bounce depth-1
                     if (ts.best >= 0) light[(depth - 1) * BLOCK] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
-                        TMPT_START_QUERY(mk(nxt[0], nxt[BLOCK], nxt[2 * BLOCK]),
-                                         mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]), false)
+                        start = true;  // the scattered ray of that bounce
+                        so = mk(nxt[0], nxt[BLOCK], nxt[2 * BLOCK]);
+                        sd = mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]);
                     } else {
                         finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
                     }
@@ -652,7 +651,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     ++smp;
                     depth = 0;
                     if (smp < (uint32_t)a.spp) {
-                        TMPT_CAMERA_SAMPLE()
+                        cam = true;
                     } else {
                         out[pix] = (COUNT && pc.cost_map)
                                        ? cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris - work0
@@ -660,6 +659,20 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         has_pix = false;
                     }
                 }
+            }
+            if (cam) {  // next camera sample of this lane's pixel (main.cpp:212-216)
+                const int lr = (int)(pix / (uint32_t)a.W);
+                const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
+                camera_sample(a.cam, (uint32_t)x, (uint32_t)tile_row_to_y(a, lr), a.invW, a.invH, rng,
+                              so, sd);
+                start = true;
+            }
+            if (start) {
+                r = make_trav_ray(so, sd);
+                trav_init(ts, kMaxT);
+                qany = sany;
+                if (sany) ++rays_s; else ++rays_e;
+                in_query = !ray_has_nan(so, sd);  // NaN: a counted miss
             }
         }
         if (!__any(in_query)) {
@@ -691,8 +704,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             }
         }
     }
-#undef TMPT_CAMERA_SAMPLE
-#undef TMPT_START_QUERY
     uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
     uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
     uint32_t nt = COUNT ? wave_sum(cnt.tris) : 0u;
@@ -997,23 +1008,25 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // default = BVH4Q octant decode
     const char* nf = getenv("TMPT_NODE");
     const int fmt = nf && nf[0] == 'q' ? 0 : (nf && nf[0] == 'f' ? 1 : 2);
+    constexpr int kSparse = 2;  // sparse-wave shading threshold divisor (k_path TAIL)
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
     PathFn fn = nullptr;
 #define TMPT_PF(C_, F_) \
-    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_>;
+    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 1, kSparse>;
     TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2)
 #undef TMPT_PF
     const bool quant = fmt == 0;
-    // TMPT_TUNE=900,<steps>,<shade_min>,<vote>: tuning variants of the path kernel
+    // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
-        int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 1;
+        int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
         if (sscanf(tune, "%d,%d,%d,%d,%d", &a0, &a1, &a2, &a3, &a4) >= 4 && a0 == 900 && !count) {
-#define TMPT_PV(ST_, SM_, V_, O_)                                                  \
-    if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == O_)                           \
-        fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, O_>               \
-                   : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, O_>     \
-                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 2, O_>);
-            TMPT_PV(4, 8, 1, 1) TMPT_PV(16, 16, 1, 1) TMPT_PV(8, 8, 1, 5)
+#define TMPT_PV(ST_, SM_, V_, T_)                                                  \
+    if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == T_)                           \
+        fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, 1, T_>            \
+                   : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, 1, T_>  \
+                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 2, 1, T_>);
+            TMPT_PV(16, 16, 1, 0) TMPT_PV(8, 8, 1, 1) TMPT_PV(8, 8, 1, 2) TMPT_PV(8, 8, 1, 4) TMPT_PV(8, 8, 2, 2)
+            TMPT_PV(16, 16, 1, 2) TMPT_PV(16, 16, 1, 4)
 #undef TMPT_PV
         }
     }

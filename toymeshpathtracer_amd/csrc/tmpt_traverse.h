@@ -18,10 +18,14 @@
 
 namespace tmpt {
 
+// 1/d for box culling only (never for a reported value): v_rcp_f32 (1 ulp).
+// The slab distances are already off the exact ones by the rounding of o/d
+// and of the fma; box padding (kBoxPadRel, ~84 ulp of the coordinates) and
+// kTfarSlack absorb both, so culling stays conservative.
 __device__ __forceinline__ float safe_inv(float d)
 {
     float a = fabsf(d) < 1e-20f ? copysignf(1e-20f, d) : d;
-    return 1.0f / a;
+    return __builtin_amdgcn_rcpf(a);
 }
 
 struct TravRay {
