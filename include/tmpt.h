@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 1
+#define TMPT_ABI_VERSION 2  /* 2: progressive spp (tmpt_render_desc.spp_begin / spp_count) */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -61,7 +61,15 @@ typedef struct {
     int32_t shard, num_shards;
     int32_t engine;
     int32_t flags;
-    int32_t reserved[7];
+    /* Progressive spp (persistent engine, pixel mode): this call runs samples
+     * [spp_begin, spp_begin + spp_count) of every pixel (spp_count 0 = to spp).
+     * A call with spp_begin > 0 continues the per-pixel state (RNG, colour sum)
+     * the previous call on this scene left for the same shard, so the passes
+     * together equal one full render bit for bit; each pass writes a preview
+     * (colour sum / samples so far, main.cpp:221-233 at that count) and the
+     * pass that reaches spp writes the final image. */
+    int32_t spp_begin, spp_count;
+    int32_t reserved[5];
 } tmpt_render_desc;
 
 /* Statistics of the last render on a scene (HIP-event timed on the scene's

@@ -254,3 +254,40 @@ def test_count_visits_instrumentation(gpu):
     c = seen[(tm.ENGINE_PERSISTENT, "f")]
     assert np.array_equal(a[0], c[0]) and c[1] == a[1] and c[2] <= a[2] and c[3] <= a[3]
     sc.close()
+
+
+# ---------------------------------------------------------------- progressive spp
+@pytest.mark.parametrize("name,w,h,spp,passes", [("suzanne.obj", 160, 90, 16, [1, 3, 4, 8]),
+                                                 ("teapot.obj", 320, 180, 8, [5, 3])])
+def test_progressive_passes_equal_full_render(gpu, name, w, h, spp, passes):
+    """Passes of spp_count samples continue each pixel's RNG stream and colour sum:
+    the last pass is the full render bit for bit, every preview equals a full
+    render at that sample count, and the passes' rays sum to the full count."""
+    tris, bmin, bmax, sc = _scene(name)
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    total = 0
+    for done, img, r in sc.trace_progressive(cam, w, h, spp, passes):
+        total += r
+        ref, _ = sc.trace_image(cam, w, h, done, seed_mode=tm.SEED_PIXEL)
+        assert np.array_equal(img, ref), done
+    assert np.array_equal(img, full) and total == rays
+    sc.close()
+
+
+def test_progressive_shards_and_errors(gpu):
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    w, h, spp = 160, 90, 6
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    full, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16, shard=1, num_shards=3)
+    *_, (done, img, _) = sc.trace_progressive(cam, w, h, spp, 2, band_rows=16, shard=1, num_shards=3)
+    assert done == spp and np.array_equal(img, full)
+    # a continuation needs the previous pass of the same shard
+    with pytest.raises(tm.TmptError, match="continue"):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=2, spp_count=2)
+    with pytest.raises(tm.TmptError, match="persistent"):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT,
+                       spp_begin=0, spp_count=2)
+    with pytest.raises(tm.TmptError, match="spp_begin"):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=6, spp_count=1)
+    sc.close()

@@ -110,3 +110,56 @@ def test_assemble_numpy():
     tiles = [np.concatenate([t, np.zeros((2, w, 4), np.uint8)]) for t in tiles]  # padded
     shard.assemble(tiles, rows, frame)
     assert np.array_equal(frame[:, 0, 0], np.arange(h))
+
+
+# ---------------------------------------------------------------- parallel host paths
+@pytest.fixture
+def small_chunks(monkeypatch):
+    """Force the parallel OBJ parser and PNG encoder to cut tiny pieces."""
+    monkeypatch.setenv("TMPT_OBJ_CHUNK", "7")
+    monkeypatch.setenv("TMPT_OBJ_THREADS", "4")
+    monkeypatch.setenv("TMPT_PNG_STRIP", "3")
+    monkeypatch.setenv("TMPT_PNG_THREADS", "4")
+
+
+@pytest.mark.parametrize("case", sorted(OBJ_CASES))
+def test_parallel_obj_chunks_match_oracle(tmp_path, small_chunks, case):
+    """Chunks cut at every few bytes (negative indices resolved across chunk
+    boundaries) give exactly the sequential parse."""
+    p = tmp_path / f"{case}.obj"
+    p.write_bytes((OBJ_CASES[case] * 3).encode())
+    a, amin, amax = tm.load_scene(str(p))
+    b, bmin, bmax = oracle.load_scene(str(p))
+    assert a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(amin.view(np.uint32), bmin.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["suzanne.obj", "teapot.obj"])
+def test_parallel_obj_files_match_oracle(small_chunks, monkeypatch, name):
+    monkeypatch.setenv("TMPT_OBJ_CHUNK", "4096")
+    a, _, _ = tm.load_scene(data(name))
+    b, _, _ = oracle.load_scene(data(name))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("h,w", [(1, 1), (2, 5), (37, 53), (200, 91)])
+def test_parallel_png_decodes_exactly(tmp_path, small_chunks, h, w):
+    rng = np.random.default_rng(h * 1000 + w)
+    img = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+    img[h // 2:] = img[h // 2:] // 17 * 17  # compressible half: long matches across strips
+    p = tmp_path / "x.png"
+    tm.write_png(str(p), img)
+    back = np.asarray(Image.open(p).convert("RGBA"))
+    assert np.array_equal(back, img[::-1])
+
+
+def test_parallel_png_same_pixels_as_sequential(tmp_path, monkeypatch):
+    img = (np.arange(120 * 77 * 4) % 251).astype(np.uint8).reshape(120, 77, 4)
+    monkeypatch.setenv("TMPT_PNG_THREADS", "1")
+    tm.write_png(str(tmp_path / "a.png"), img)
+    monkeypatch.setenv("TMPT_PNG_THREADS", "8")
+    monkeypatch.setenv("TMPT_PNG_STRIP", "5")
+    tm.write_png(str(tmp_path / "b.png"), img)
+    a = np.asarray(Image.open(tmp_path / "a.png").convert("RGBA"))
+    b = np.asarray(Image.open(tmp_path / "b.png").convert("RGBA"))
+    assert np.array_equal(a, b) and np.array_equal(a, img[::-1])

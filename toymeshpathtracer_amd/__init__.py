@@ -79,7 +79,8 @@ class _Desc(ctypes.Structure):
                 ("seed_mode", ctypes.c_int32), ("band_rows", ctypes.c_int32),
                 ("shard", ctypes.c_int32), ("num_shards", ctypes.c_int32),
                 ("engine", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7)]
+                ("spp_begin", ctypes.c_int32), ("spp_count", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class _Stats(ctypes.Structure):
@@ -252,11 +253,12 @@ class RenderStats:
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
-          engine=ENGINE_PERSISTENT, flags=0) -> _Desc:
+          engine=ENGINE_PERSISTENT, flags=0, spp_begin=0, spp_count=0) -> _Desc:
     d = _Desc()
     d.width, d.height, d.spp, d.seed_mode = width, height, spp, seed_mode
     d.band_rows, d.shard, d.num_shards = band_rows, shard, num_shards
     d.engine, d.flags = engine, flags
+    d.spp_begin, d.spp_count = spp_begin, spp_count
     return d
 
 
@@ -323,12 +325,15 @@ class Scene:
     def trace_image(self, camera: Camera, width: int, height: int, spp: int,
                     seed_mode: int = SEED_ROW, engine: int = ENGINE_PERSISTENT, band_rows: int = 0,
                     shard: int = 0, num_shards: int = 1, count_visits: bool = False,
-                    out=None) -> Tuple[np.ndarray, int]:
+                    out=None, spp_begin: int = 0, spp_count: int = 0) -> Tuple[np.ndarray, int]:
         """Render one shard.  Returns (rgba[tile_rows, width, 4] uint8, rays).
         Row 0 is the lowest rendered row (main.cpp:229; flipped on PNG write).
-        ``out`` may be a device pointer (int) with tile_rows*width*4 bytes."""
+        ``out`` may be a device pointer (int) with tile_rows*width*4 bytes.
+        ``spp_begin``/``spp_count``: one progressive pass (persistent engine,
+        pixel seeding) -- see :meth:`trace_progressive`."""
         d = _desc(width, height, spp, seed_mode, band_rows, shard, num_shards, engine,
-                  (FLAG_COUNT_VISITS if count_visits else 0) | (FLAG_OUT_DEVICE if out is not None else 0))
+                  (FLAG_COUNT_VISITS if count_visits else 0) | (FLAG_OUT_DEVICE if out is not None else 0),
+                  spp_begin, spp_count)
         rows = int(_tile_rows(ctypes.byref(d)))
         rays = ctypes.c_uint64()
         cam = camera._to_c()
@@ -340,6 +345,23 @@ class Scene:
         _check(_render(self._h, ctypes.byref(cam), ctypes.byref(d), img.ctypes.data_as(ctypes.c_void_p),
                        ctypes.byref(rays)), "trace_image")
         return img, int(rays.value)
+
+    def trace_progressive(self, camera: Camera, width: int, height: int, spp: int, passes,
+                          band_rows: int = 0, shard: int = 0, num_shards: int = 1):
+        """Progressive spp: yields (samples_done, preview rgba, rays of the pass) per
+        pass; ``passes`` = samples per pass (int) or a list of them summing to spp.
+        The last preview is the final image, bit-identical to one full render."""
+        if isinstance(passes, int):
+            passes = [min(passes, spp - b) for b in range(0, spp, passes)]
+        if sum(passes) != spp or min(passes) < 1:
+            raise ValueError("passes must be positive and sum to spp")
+        done = 0
+        for n in passes:
+            img, rays = self.trace_image(camera, width, height, spp, seed_mode=SEED_PIXEL,
+                                         engine=ENGINE_PERSISTENT, band_rows=band_rows, shard=shard,
+                                         num_shards=num_shards, spp_begin=done, spp_count=n)
+            done += n
+            yield done, img, rays
 
     def stats(self) -> RenderStats:
         s = _Stats()

@@ -154,6 +154,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.nodes) (void)hipFree(s.nodes);
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.nodes4f) (void)hipFree(s.nodes4f);
+    if (s.prog) (void)hipFree(s.prog);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);
@@ -233,6 +234,12 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
         return bad("tmpt_render: invalid engine");
     if (d->num_shards > 1 && (d->shard < 0 || d->shard >= d->num_shards))
         return bad("tmpt_render: invalid shard");
+    if (d->spp_begin < 0 || d->spp_begin >= d->spp || d->spp_count < 0 ||
+        d->spp_count > d->spp - d->spp_begin)
+        return bad("tmpt_render: invalid spp_begin / spp_count");
+    const bool progressive = d->spp_begin > 0 || (d->spp_count > 0 && d->spp_count < d->spp);
+    if (progressive && (d->engine != TMPT_ENGINE_PERSISTENT || d->seed_mode != TMPT_SEED_PIXEL))
+        return bad("tmpt_render: progressive spp needs the persistent engine and pixel seeding");
     Scene& s = h->s;
     TMPT_HIP(hipSetDevice(s.device));
     const int32_t rows = tmpt_tile_rows(d);

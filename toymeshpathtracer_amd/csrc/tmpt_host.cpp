@@ -18,8 +18,11 @@
 #include <string.h>
 #include <zlib.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tmpt.h"
@@ -103,8 +106,78 @@ int read_face_vertex(Cursor& c)
     return vi;
 }
 
+// Environment knobs of the parallel host paths (tests force small chunks).
+int env_int(const char* name, int dflt)
+{
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+int host_threads(const char* env)
+{
+    int t = env_int(env, 0);
+    if (t > 0) return t;
+    unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hw));
+}
+
+// One text chunk of an OBJ file parsed on its own: positions, and faces whose
+// negative (relative) indices are resolved against the chunk-local vertex
+// count and fixed up once the vertex counts of the earlier chunks are known.
+struct ObjChunk {
+    std::vector<float> pos;
+    std::vector<int32_t> faces;
+    std::vector<uint32_t> rel;  // indices into faces holding chunk-relative values
+};
+
+void parse_obj_chunk(const char* p, const char* end, ObjChunk& out)
+{
+    while (p < end) {
+        const char* eol = (const char*)memchr(p, '\n', (size_t)(end - p));
+        const char* le = eol ? eol : end;
+        Cursor c{p, le};
+        if (le - p >= 2 && p[0] == 'v' && p[1] == ' ') {
+            c.p += 2;
+            float x = read_float(c), y = read_float(c), z = read_float(c);
+            out.pos.push_back(x);
+            out.pos.push_back(y);
+            out.pos.push_back(z);
+        } else if (le - p >= 2 && p[0] == 'f' && p[1] == ' ') {
+            c.p += 2;
+            const int nv = (int)(out.pos.size() / 3);
+            int fan0 = 0, prev = 0, k = 0;
+            bool rfan0 = false, rprev = false;
+            while (c.p < c.end) {
+                int vi = read_face_vertex(c);
+                if (vi == 0) break;
+                const bool r = vi < 0;
+                int idx = r ? nv + vi : vi - 1;  // objparser.cpp:29-32 (rel: + chunk base)
+                if (k == 0) {
+                    fan0 = idx;
+                    rfan0 = r;
+                } else if (k >= 2) {
+                    const int v3[3] = {fan0, prev, idx};
+                    const bool r3[3] = {rfan0, rprev, r};
+                    for (int j = 0; j < 3; ++j) {
+                        if (r3[j]) out.rel.push_back((uint32_t)out.faces.size());
+                        out.faces.push_back(v3[j]);
+                    }
+                }
+                prev = idx;
+                rprev = r;
+                ++k;
+            }
+        }
+        p = le + 1;
+    }
+}
+
 }  // namespace
 
+// objParseFile (objparser.cpp:304-355) + the triangle gather of LoadScene,
+// parallel: the text is cut at line starts into chunks parsed concurrently;
+// chunk results are concatenated in file order, so the triangles are exactly
+// those of a sequential parse ("parallel OBJ ingest").
 int load_obj(const char* path, std::vector<float>& tris, f3& bmin, f3& bmax)
 {
     FILE* f = fopen(path, "rb");
@@ -113,44 +186,65 @@ int load_obj(const char* path, std::vector<float>& tris, f3& bmin, f3& bmax)
         return -1;
     }
     std::string text;
-    char buf[1 << 16];
-    size_t got;
-    while ((got = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, got);
+    if (fseek(f, 0, SEEK_END) == 0) {
+        long sz = ftell(f);
+        if (sz > 0) text.resize((size_t)sz);
+        fseek(f, 0, SEEK_SET);
+    }
+    size_t got = text.empty() ? 0 : fread(&text[0], 1, text.size(), f);
+    text.resize(got);
+    {  // files whose size ftell cannot tell (pipes): read to the end
+        char buf[1 << 16];
+        size_t more;
+        while ((more = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, more);
+    }
     fclose(f);
 
-    std::vector<float> pos;      // xyz per vertex
-    std::vector<int32_t> faces;  // 3 position indices per triangle (0-based)
-    const char* p = text.data();
-    const char* end = p + text.size();
-    while (p < end) {
-        const char* eol = (const char*)memchr(p, '\n', (size_t)(end - p));
-        const char* le = eol ? eol : end;
-        Cursor c{p, le};
-        if (le - p >= 2 && p[0] == 'v' && p[1] == ' ') {
-            c.p += 2;
-            float x = read_float(c), y = read_float(c), z = read_float(c);
-            pos.push_back(x);
-            pos.push_back(y);
-            pos.push_back(z);
-        } else if (le - p >= 2 && p[0] == 'f' && p[1] == ' ') {
-            c.p += 2;
-            const int nv = (int)(pos.size() / 3);
-            int fan0 = 0, prev = 0, k = 0;
-            while (c.p < c.end) {
-                int vi = read_face_vertex(c);
-                if (vi == 0) break;
-                int idx = vi >= 0 ? vi - 1 : nv + vi;  // objparser.cpp:29-32
-                if (k == 0) fan0 = idx;
-                else if (k >= 2) {
-                    faces.push_back(fan0);
-                    faces.push_back(prev);
-                    faces.push_back(idx);
-                }
-                prev = idx;
-                ++k;
-            }
+    const char* base = text.data();
+    const size_t len = text.size();
+    const size_t min_chunk = (size_t)std::max(1, env_int("TMPT_OBJ_CHUNK", 1 << 20));
+    const int nthreads = host_threads("TMPT_OBJ_THREADS");
+    size_t nchunks = std::max<size_t>(1, std::min<size_t>((size_t)nthreads * 4, len / min_chunk));
+    std::vector<size_t> cut(nchunks + 1, len);
+    cut[0] = 0;
+    for (size_t k = 1; k < nchunks; ++k) {  // chunk k starts at the line after byte k*len/n
+        size_t at = std::max(cut[k - 1], k * len / nchunks);
+        const char* nl = at < len ? (const char*)memchr(base + at, '\n', len - at) : nullptr;
+        cut[k] = nl ? (size_t)(nl - base) + 1 : len;
+    }
+    std::vector<ObjChunk> chunks(nchunks);
+    {
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t k; (k = next.fetch_add(1)) < nchunks;)
+                parse_obj_chunk(base + cut[k], base + cut[k + 1], chunks[k]);
+        };
+        std::vector<std::thread> pool;
+        const int nt = (int)std::min<size_t>((size_t)nthreads, nchunks);
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+        work();
+        for (auto& t : pool) t.join();
+    }
+    std::vector<float> pos;
+    std::vector<int32_t> faces;
+    {
+        size_t np = 0, nf = 0;
+        for (auto& ch : chunks) {
+            np += ch.pos.size();
+            nf += ch.faces.size();
         }
-        p = le + 1;
+        pos.reserve(np);
+        faces.reserve(nf);
+        int32_t vbase = 0;
+        for (auto& ch : chunks) {
+            const size_t f0 = faces.size();
+            pos.insert(pos.end(), ch.pos.begin(), ch.pos.end());
+            faces.insert(faces.end(), ch.faces.begin(), ch.faces.end());
+            for (uint32_t r : ch.rel) faces[f0 + r] += vbase;
+            vbase += (int32_t)(ch.pos.size() / 3);
+            std::vector<float>().swap(ch.pos);
+            std::vector<int32_t>().swap(ch.faces);
+        }
     }
     // LoadScene, main.cpp:132-162
     const size_t n = faces.size() / 3;
@@ -242,23 +336,122 @@ void chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data, size_
     uint32_t crc = (uint32_t)crc32(0L, o.data() + start, (uInt)(len + 4));
     be32(o, crc);
 }
+
+// PNG filter choice per row as stb_image_write does it (minimum sum of
+// absolute filtered bytes over the five filters, PNG spec 9.2-9.4).
+void filter_row(const uint8_t* cur, const uint8_t* up, int bytes, uint8_t* dst)
+{
+    static thread_local std::vector<uint8_t> tmp;
+    tmp.resize((size_t)bytes);
+    int best_sum = -1;
+    for (int ft = 0; ft < 5; ++ft) {
+        int sum = 0;
+        for (int i = 0; i < bytes; ++i) {
+            const int a = i >= 4 ? cur[i - 4] : 0, b = up ? up[i] : 0, c = (up && i >= 4) ? up[i - 4] : 0;
+            int pred = 0;
+            switch (ft) {
+                case 1: pred = a; break;
+                case 2: pred = b; break;
+                case 3: pred = (a + b) >> 1; break;
+                case 4: {
+                    const int pp = a + b - c, pa = abs(pp - a), pb = abs(pp - b), pc = abs(pp - c);
+                    pred = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+                    break;
+                }
+                default: break;
+            }
+            const uint8_t v = (uint8_t)(cur[i] - pred);
+            tmp[(size_t)i] = v;
+            sum += (int8_t)v < 0 ? -(int8_t)v : (int8_t)v;
+        }
+        if (best_sum < 0 || sum < best_sum) {
+            best_sum = sum;
+            dst[0] = (uint8_t)ft;
+            memcpy(dst + 1, tmp.data(), (size_t)bytes);
+        }
+    }
+}
+
 }  // namespace
 
+// stbi_write_png + flip (main.cpp:341-342), parallel:
+// rows are filtered and deflated in strips on host threads; each strip is a
+// raw deflate stream ending on a byte boundary (Z_SYNC_FLUSH; the last one
+// Z_FINISH) primed with the previous strip's last 32 KiB as its dictionary, so
+// the strips concatenate into ONE zlib stream (adler32 combined) -- a single
+// ordinary IDAT any decoder reads.  Threads: TMPT_PNG_THREADS (1 = sequential).
 int write_png(const char* path, const uint8_t* rgba, int w, int h)
 {
-    // rows are written top-down from the bottom-up image (stbi flip, main.cpp:341)
-    std::vector<uint8_t> raw((size_t)h * ((size_t)w * 4 + 1));
-    for (int r = 0; r < h; ++r) {
-        uint8_t* dst = &raw[(size_t)r * ((size_t)w * 4 + 1)];
-        dst[0] = 0;  // filter: none
-        memcpy(dst + 1, rgba + (size_t)(h - 1 - r) * w * 4, (size_t)w * 4);
+    const size_t stride = (size_t)w * 4 + 1;
+    std::vector<uint8_t> raw((size_t)h * stride);
+    // file row r (top-down) = image row h-1-r (bottom-up, stbi flip)
+    auto img_row = [&](int r) { return rgba + (size_t)(h - 1 - r) * (size_t)w * 4; };
+    const int nthreads = host_threads("TMPT_PNG_THREADS");
+    const int strip_rows = std::max(1, env_int("TMPT_PNG_STRIP", 64));
+    const int nstrips = std::max(1, (h + strip_rows - 1) / strip_rows);
+    std::vector<std::vector<uint8_t>> zs((size_t)nstrips);
+    std::vector<uLong> adl((size_t)nstrips);
+    std::atomic<int> next{0};
+    std::atomic<bool> failed{false};
+    auto work = [&]() {
+        for (int k; (k = next.fetch_add(1)) < nstrips;) {
+            const int r0 = k * strip_rows, r1 = std::min(h, r0 + strip_rows);
+            for (int r = r0; r < r1; ++r)
+                filter_row(img_row(r), r > 0 ? img_row(r - 1) : nullptr, w * 4, &raw[(size_t)r * stride]);
+            const uint8_t* src = &raw[(size_t)r0 * stride];
+            const size_t n = (size_t)(r1 - r0) * stride;
+            adl[(size_t)k] = adler32(adler32(0L, Z_NULL, 0), src, (uInt)n);
+            z_stream zs_{};
+            if (deflateInit2(&zs_, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+                failed = true;
+                continue;
+            }
+            if (k > 0) {
+                // dictionary = the last 32 KiB of the previous strip's filtered rows;
+                // another thread may be writing those into `raw`, so filter them here
+                const int need = (int)((32768 + stride - 1) / stride);
+                const int p0 = std::max(0, r0 - std::min(strip_rows, need));
+                std::vector<uint8_t> prev((size_t)(r0 - p0) * stride);
+                for (int r = p0; r < r0; ++r)
+                    filter_row(img_row(r), r > 0 ? img_row(r - 1) : nullptr, w * 4,
+                               &prev[(size_t)(r - p0) * stride]);
+                const size_t dn = std::min<size_t>(prev.size(), 32768);
+                deflateSetDictionary(&zs_, prev.data() + prev.size() - dn, (uInt)dn);
+            }
+            std::vector<uint8_t>& out = zs[(size_t)k];
+            out.resize(deflateBound(&zs_, (uLong)n) + 16);
+            zs_.next_in = const_cast<Bytef*>(src);
+            zs_.avail_in = (uInt)n;
+            zs_.next_out = out.data();
+            zs_.avail_out = (uInt)out.size();
+            const int rc = deflate(&zs_, k == nstrips - 1 ? Z_FINISH : Z_SYNC_FLUSH);
+            if ((k == nstrips - 1 && rc != Z_STREAM_END) || (k < nstrips - 1 && rc != Z_OK)) failed = true;
+            out.resize(out.size() - zs_.avail_out);
+            deflateEnd(&zs_);
+        }
+    };
+    {
+        std::vector<std::thread> pool;
+        const int nt = std::min(nthreads, nstrips);
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+        work();
+        for (auto& t : pool) t.join();
     }
-    uLongf zlen = compressBound((uLong)raw.size());
-    std::vector<uint8_t> z(zlen);
-    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) {
+    if (failed) {
         set_error("png: deflate failed");
         return -1;
     }
+    std::vector<uint8_t> z = {0x78, 0x9C};  // zlib header: deflate, 32 KiB window, default level
+    uLong ad = adl[0];
+    for (int k = 0; k < nstrips; ++k) {
+        z.insert(z.end(), zs[(size_t)k].begin(), zs[(size_t)k].end());
+        if (k > 0) {
+            const int r0 = k * strip_rows, r1 = std::min(h, r0 + strip_rows);
+            ad = adler32_combine(ad, adl[(size_t)k], (z_off_t)((size_t)(r1 - r0) * stride));
+        }
+    }
+    be32(z, (uint32_t)ad);
+    const uLongf zlen = (uLongf)z.size();
     std::vector<uint8_t> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
     uint8_t ihdr[13];
     ihdr[0] = (uint8_t)(w >> 24); ihdr[1] = (uint8_t)(w >> 16); ihdr[2] = (uint8_t)(w >> 8); ihdr[3] = (uint8_t)w;

@@ -102,6 +102,11 @@ struct Scene {
     // render workspace (grown on demand, reused across calls)
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    // progressive spp: per-pixel {colour sum xyz, rng} of the last pass, and the
+    // shard it belongs to (width, height, spp, band_rows, shard, num_shards, next sample)
+    float4* prog = nullptr;
+    size_t prog_slots = 0;
+    int32_t prog_key[7] = {0, 0, 0, 0, 0, 0, -1};
     // statistics of the last render
     double render_ms = 0.0;
     double extend_ms = 0.0;

@@ -16,6 +16,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <chrono>
@@ -32,6 +33,11 @@ struct RenderArgs {
     int32_t W, H, spp, seed_mode, band_rows, shard, nshards, tile_rows;
     float invW, invH, spp_recip;
     int64_t slots;  // tile_rows * W
+    // progressive spp: samples [smp_begin, smp_end) this call; prog = per-pixel
+    // {colour sum, rng} carried between calls (null: one full pass)
+    int32_t smp_begin, smp_end;
+    float out_recip;  // 1/spp for the final pass, 1/smp_end for a preview
+    float4* prog;
 };
 
 __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
@@ -602,10 +608,16 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                    rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
-                    smp = 0;
+                    if (a.smp_begin == 0) {
+                        rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
+                        col = mk(0.0f, 0.0f, 0.0f);
+                    } else {  // progressive: continue the previous pass's stream and sum
+                        const float4 pv = a.prog[pix];
+                        col = mk(pv.x, pv.y, pv.z);
+                        rng = __float_as_uint(pv.w);
+                    }
+                    smp = (uint32_t)a.smp_begin;
                     depth = 0;
-                    col = mk(0.0f, 0.0f, 0.0f);
                     if (COUNT) work0 = cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
                     cam = true;
                 }
@@ -650,12 +662,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     col = col + color;
                     ++smp;
                     depth = 0;
-                    if (smp < (uint32_t)a.spp) {
+                    if (smp < (uint32_t)a.smp_end) {
                         cam = true;
                     } else {
+                        if (a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
                         out[pix] = (COUNT && pc.cost_map)
                                        ? cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris - work0
-                                       : pack_pixel(col, a.spp_recip);
+                                       : pack_pixel(col, a.out_recip);
                         has_pix = false;
                     }
                 }
@@ -786,6 +799,10 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     a.invH = 1.0f / (float)d->height;            // main.cpp:187
     a.spp_recip = 1.0f / (float)d->spp;          // main.cpp:188
     a.slots = (int64_t)a.tile_rows * a.W;
+    a.smp_begin = d->spp_begin;
+    a.smp_end = d->spp_count > 0 ? d->spp_begin + d->spp_count : d->spp;
+    a.out_recip = a.smp_end == d->spp ? a.spp_recip : 1.0f / (float)a.smp_end;
+    a.prog = nullptr;
     return a;
 }
 
@@ -1077,6 +1094,26 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     }
     RenderArgs a = make_args(cam, d);
     bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
+    // progressive spp: keep per-pixel state for the shard between calls
+    const bool progressive = a.smp_begin > 0 || a.smp_end < a.spp;
+    if (progressive) {
+        const int32_t key[6] = {d->width, d->height, d->spp, a.band_rows, a.shard, a.nshards};
+        if (a.smp_begin > 0 &&
+            (memcmp(key, s.prog_key, sizeof(key)) != 0 || s.prog_key[6] != a.smp_begin)) {
+            set_error("tmpt_render: spp_begin does not continue the previous pass of this shard");
+            return -22;
+        }
+        if (s.prog_slots < (size_t)a.slots) {
+            if (s.prog) (void)hipFree(s.prog);
+            s.prog = nullptr;
+            s.prog_slots = 0;
+            TMPT_HIP(hipMalloc(&s.prog, sizeof(float4) * (size_t)a.slots));
+            s.prog_slots = (size_t)a.slots;
+        }
+        a.prog = s.prog;
+        memcpy(s.prog_key, key, sizeof(key));
+        s.prog_key[6] = -1;  // valid again only once this pass completes
+    }
     unsigned long long* d_counters = nullptr;
     constexpr int kCounters = 16;
     TMPT_HIP(hipMallocAsync((void**)&d_counters, kCounters * sizeof(unsigned long long), s.stream));
@@ -1088,6 +1125,13 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     int rc = 0;
     bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode == TMPT_SEED_PIXEL;
     bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_PIXEL && use_wide();
+    if (progressive && !persistent) {
+        set_error("tmpt_render: progressive spp needs the persistent engine (TMPT_BVH=2 is BVH2-only)");
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipFreeAsync(d_counters, s.stream);
+        return -22;
+    }
     s.extend_ms = s.shadow_ms = 0;
     s.extend_rays = s.shadow_rays = s.node_visits = s.tri_tests = 0;
     s.shadow_node_visits = s.shadow_tri_tests = 0;
@@ -1113,6 +1157,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         return -1;
     }
     s.render_ms = ms;
+    if (progressive) s.prog_key[6] = a.smp_end < a.spp ? a.smp_end : -1;
     if (persistent) {  // one kernel for both query kinds
         s.extend_ms = ms;
         s.extend_rays = c[3];
