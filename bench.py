@@ -240,8 +240,14 @@ def main() -> None:
                                 row_step=args.cpu_row_step, threads=threads)
         cdt = time.perf_counter() - t1
         rows = np.arange(0, H, args.cpu_row_step)
+        cpu_model = ""
+        try:
+            with open("/proc/cpuinfo") as f:
+                cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+        except OSError:
+            pass
         cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads,
-               "kind": "port",
+               "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model,
                "sample": f"rows y%{args.cpu_row_step}==0 ({len(rows)} x {W} px x {SPP} spp, "
                          f"{crays} rays, {cdt:.1f} s), octree restatement of scene.cpp, pixel seeding"}
         diff = int((frame[rows] != ref[rows]).any(-1).sum())
@@ -250,6 +256,35 @@ def main() -> None:
 
     if args.save:
         tm.write_png(args.save, frame)
+
+    # ---- host paths either side of the hot path: OBJ
+    # ingest and PNG encode, sequential vs parallel (off the timed region, as in
+    # main.cpp:122-170 / 341-342)
+    host = None
+    if rank == 0:
+        import tempfile
+
+        def timed(fn, env, val):
+            old = os.environ.get(env)
+            os.environ[env] = str(val)
+            try:
+                t = time.perf_counter()
+                fn()
+                return round((time.perf_counter() - t) * 1e3, 2)
+            finally:
+                if old is None:
+                    del os.environ[env]
+                else:
+                    os.environ[env] = old
+
+        png = os.path.join(tempfile.gettempdir(), f"tmpt_bench_{os.getpid()}.png")
+        nt = min(16, os.cpu_count() or 1)
+        host = {"obj_parse_ms": {"threads_1": timed(lambda: tm.load_scene(path), "TMPT_OBJ_THREADS", 1),
+                                 f"threads_{nt}": timed(lambda: tm.load_scene(path), "TMPT_OBJ_THREADS", nt)},
+                "png_encode_ms": {"threads_1": timed(lambda: tm.write_png(png, frame), "TMPT_PNG_THREADS", 1),
+                                  f"threads_{nt}": timed(lambda: tm.write_png(png, frame), "TMPT_PNG_THREADS", nt)},
+                "obj_bytes": os.path.getsize(path), "png_bytes": os.path.getsize(png)}
+        os.remove(png)
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "MRays/s", "n_gpus": world,
@@ -263,7 +298,7 @@ def main() -> None:
                    "seed_mode": "pixel", "engine": args.engine,
                    "parallelism": f"row-bands{BAND_ROWS}x{world}",
                    "rays_per_step": rays // args.steps},
-        "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity,
+        "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "host_paths": host,
         "scene_init_s": round(init_s, 3), "bvh_build_ms": round(st0.build_ms, 2),
         "bvh": {"lbvh2_depth": st0.bvh_depth, "bvh4_nodes": st0.bvh4_nodes, "bvh4_depth": st0.bvh4_depth,
                 "leaf_max": st0.leaf_max, "builder": "ploc" if st0.builder_iters else "lbvh",

@@ -48,6 +48,16 @@ __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// s_memtime (shader clock), for the PROF build of k_path only
+__device__ __forceinline__ uint64_t stamp()
+{
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
 // wave64 sum of a 32-bit value (all lanes must call)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
@@ -526,7 +536,7 @@ struct PathCtl {
 };
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
-          int OCC = 1, int TAIL = 0>
+          int OCC = 1, int TAIL = 0, int PROF = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -552,6 +562,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
     // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
     uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
+    // PROF: wave-uniform s_memtime cycles in shading rounds, node rounds, leaf rounds
+    uint64_t pt_shade = 0, pt_node = 0, pt_leaf = 0, pt_t = PROF ? stamp() : 0;
     f3 col = mk(0.0f, 0.0f, 0.0f);
     TravRay r;
     TravState ts;
@@ -688,6 +700,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 in_query = !ray_has_nan(so, sd);  // NaN: a counted miss
             }
         }
+        if (PROF) {
+            const uint64_t t = stamp();
+            pt_shade += t - pt_t;
+            pt_t = t;
+        }
         if (!__any(in_query)) {
             if (exhausted && !__any(has_pix)) break;
             continue;
@@ -715,6 +732,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     in_query = false;
                 }
             }
+            if (PROF) {
+                const uint64_t t = stamp();
+                (leaf_round && vote ? pt_leaf : pt_node) += t - pt_t;
+                pt_t = t;
+            }
         }
     }
     uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
@@ -737,6 +759,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             atomicAdd(&counters[10], (unsigned long long)rs_sr);
             atomicAdd(&counters[11], (unsigned long long)rs_sl);
             atomicAdd(&counters[12], (unsigned long long)rs_st);
+        }
+        if (PROF) {
+            atomicAdd(&counters[13], (unsigned long long)pt_shade);
+            atomicAdd(&counters[14], (unsigned long long)pt_node);
+            atomicAdd(&counters[15], (unsigned long long)pt_leaf);
         }
     }
 }
@@ -1033,6 +1060,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2)
 #undef TMPT_PF
     const bool quant = fmt == 0;
+    // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
+    const char* pe = getenv("TMPT_PROF");
+    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 2;
+    if (prof) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2, 1, kSparse, 1>;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
         int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
@@ -1168,6 +1199,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.shadow_tri_tests = c[5];
         s.extend_launches = 1;
         s.iterations = 1;
+        if (c[13] + c[14] + c[15]) {
+            const double tot = (double)(c[13] + c[14] + c[15]);
+            fprintf(stderr, "k_path wave time: shading %.1f%%, node rounds %.1f%%, leaf rounds %.1f%% "
+                            "(%.3g wave-cycles)\n",
+                    100.0 * c[13] / tot, 100.0 * c[14] / tot, 100.0 * c[15] / tot, tot);
+        }
         if (count && getenv("TMPT_ROUND_LOG"))  // diagnostic: wave-round efficiency
             fprintf(stderr,
                     "k_path rounds: node %llu (%.1f lanes), leaf %llu (%.1f lanes), shade %llu "
