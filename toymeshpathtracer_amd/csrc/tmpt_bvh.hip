@@ -701,7 +701,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
         const uint32_t* tvals = vi;
         int troot = n == 1 ? ~0 : 0;
         if (ploc) {
-            int r = 24;
+            int r = 32;  // search radius; node visits vs r measured in DESIGN.md
             if (const char* e = getenv("TMPT_PLOC_R")) r = std::max(1, std::min(256, atoi(e)));
             int32_t* cidA = (int32_t*)alloc(nn * 4);
             int32_t* cidB = (int32_t*)alloc(nn * 4);

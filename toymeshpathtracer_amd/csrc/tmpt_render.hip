@@ -1048,22 +1048,24 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                       unsigned long long* d_counters)
 {
     constexpr int kPathSL = 16, kPathSteps = 8, kShadeMin = 8;
-    // node format (TMPT_NODE, A/B): q = BVH4Q min/max decode, f = BVH4F f32 boxes,
-    // default = BVH4Q octant decode
+    // node step (TMPT_NODE, A/B): q = BVH4Q min/max decode, f = BVH4F f32 boxes,
+    // s = BVH4Q octant decode + full near-to-far sort, default = octant decode,
+    // nearest child first (others pairwise ordered)
     const char* nf = getenv("TMPT_NODE");
-    const int fmt = nf && nf[0] == 'q' ? 0 : (nf && nf[0] == 'f' ? 1 : 2);
+    const int fmt = nf && nf[0] == 'q' ? 0 : (nf && nf[0] == 'f' ? 1 : (nf && nf[0] == 's' ? 2 : 3));
     constexpr int kSparse = 2;  // sparse-wave shading threshold divisor (k_path TAIL)
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
     PathFn fn = nullptr;
 #define TMPT_PF(C_, F_) \
     if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 1, kSparse>;
-    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2)
+    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3)
+    TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3)
 #undef TMPT_PF
     const bool quant = fmt == 0;
     // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
     const char* pe = getenv("TMPT_PROF");
-    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 2;
-    if (prof) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2, 1, kSparse, 1>;
+    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 3;
+    if (prof) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 1>;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
         int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
@@ -1072,7 +1074,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == T_)                           \
         fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, 1, T_>            \
                    : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, 1, T_>  \
-                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 2, 1, T_>);
+                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 3, 1, T_>);
             TMPT_PV(16, 16, 1, 0) TMPT_PV(8, 8, 1, 1) TMPT_PV(8, 8, 1, 2) TMPT_PV(8, 8, 1, 4) TMPT_PV(8, 8, 2, 2)
             TMPT_PV(16, 16, 1, 2) TMPT_PV(16, 16, 1, 4)
 #undef TMPT_PV

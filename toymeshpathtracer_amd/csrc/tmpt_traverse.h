@@ -457,7 +457,7 @@ __device__ __forceinline__ bool trav_step4f_mixed(const SceneView& sv, const Tra
 // child pairs, no per-child min/max and no mask test (empty slots carry an
 // inverted box and link to the null leaf).  4 loads per node (the TA cost of a
 // divergent gather scales with bytes per lane) at ~BVH4F's VALU count.
-template <bool COUNT, int BLOCK, int SL>
+template <bool COUNT, int BLOCK, int SL, int SORTK = 0>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt)
@@ -504,9 +504,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             float tf = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], ts.bt));
             key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
         }
-        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
-                 (key[3] != INFINITY);
-        if (nh > 0) {
+        if (SORTK == 0) {  // all hit children near to far (misses sort last as +inf)
 #define TMPT_CSWAP(i, j)                                            \
     if (key[j] < key[i]) {                                          \
         float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
@@ -514,11 +512,29 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
     }
             TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
 #undef TMPT_CSWAP
-            if (nh > 3) st.push(ts.sp, ch[3]);
-            if (nh > 2) st.push(ts.sp, ch[2]);
-            if (nh > 1) st.push(ts.sp, ch[1]);
-            ts.node = ch[0];
-            return false;
+            if (key[0] != INFINITY) {
+                if (key[3] != INFINITY) st.push(ts.sp, ch[3]);
+                if (key[2] != INFINITY) st.push(ts.sp, ch[2]);
+                if (key[1] != INFINITY) st.push(ts.sp, ch[1]);
+                ts.node = ch[0];
+                return false;
+            }
+        } else {  // nearest child next; the others pushed pairwise-ordered only
+            const bool s01 = key[1] < key[0], s23 = key[3] < key[2];
+            const float ka = s01 ? key[1] : key[0], kao = s01 ? key[0] : key[1];
+            const int ca = s01 ? ch[1] : ch[0], cao = s01 ? ch[0] : ch[1];
+            const float kb = s23 ? key[3] : key[2], kbo = s23 ? key[2] : key[3];
+            const int cb = s23 ? ch[3] : ch[2], cbo = s23 ? ch[2] : ch[3];
+            const bool sab = kb < ka;
+            const float kn = sab ? kb : ka, kno = sab ? ka : kb;
+            const int cn = sab ? cb : ca, cno = sab ? ca : cb;
+            if (kn != INFINITY) {
+                if (kbo != INFINITY) st.push(ts.sp, cbo);
+                if (kao != INFINITY) st.push(ts.sp, cao);
+                if (kno != INFINITY) st.push(ts.sp, cno);
+                ts.node = cn;
+                return false;
+            }
         }
     } else {
         const uint32_t code = (uint32_t)ts.node;
@@ -554,7 +570,8 @@ __device__ __forceinline__ bool trav_step_fmt(const SceneView& sv, const TravRay
                                               TravState& ts, TravStack<BLOCK, SL>& st, TravCount& cnt)
 {
     if (FMT == 1) return trav_step4f_mixed<COUNT>(sv, r, any, ts, st, cnt);
-    if (FMT == 2) return trav_step4q2_mixed<COUNT>(sv, r, any, ts, st, cnt);
+    if (FMT == 2) return trav_step4q2_mixed<COUNT, BLOCK, SL, 0>(sv, r, any, ts, st, cnt);
+    if (FMT == 3) return trav_step4q2_mixed<COUNT, BLOCK, SL, 1>(sv, r, any, ts, st, cnt);
     return trav_step4_mixed<COUNT>(sv, r, any, ts, st, cnt);
 }
 
