@@ -27,7 +27,8 @@ def main():
     for name, calls, tot, avg, pct in c.execute(
             "select name,total_calls,total_duration,average,percentage from top_kernels "
             "order by total_duration desc limit 25"):
-        print(f"{short(name):<92} {calls:>6} {tot / 1e6:>10.3f} {avg / 1e6:>10.4f} {pct:>6.2f}")
+        # top_kernels durations are in microseconds
+        print(f"{short(name):<92} {calls:>6} {tot / 1e3:>10.3f} {avg / 1e3:>10.4f} {pct:>6.2f}")
     for p in pmcs:
         c = sqlite3.connect(p)
         print(f"\n# PMC: {p}")
