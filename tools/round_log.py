@@ -23,3 +23,7 @@ for n in shards:
     st = sc.stats()
     print(f"shards {n}: rays {rays} nodes {st.node_visits + st.shadow_node_visits} "
           f"tris {st.tri_tests + st.shadow_tri_tests} render {st.render_ms:.1f} ms", flush=True)
+    print(f"  closest-hit: {st.extend_rays} rays, {st.node_visits / st.extend_rays:.2f} nodes + "
+          f"{st.tri_tests / st.extend_rays:.2f} tris per ray; shadow: {st.shadow_rays} rays, "
+          f"{st.shadow_node_visits / max(st.shadow_rays, 1):.2f} nodes + "
+          f"{st.shadow_tri_tests / max(st.shadow_rays, 1):.2f} tris per ray", flush=True)
