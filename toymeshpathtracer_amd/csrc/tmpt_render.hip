@@ -48,6 +48,11 @@ __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// wave64 ballot straight from the predicate (HIP's __ballot widens the bool to
+// an int and compares it again: two extra VALU per call in the hot loops)
+__device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 // s_memtime (shader clock), for the PROF build of k_path only
 __device__ __forceinline__ uint64_t stamp()
 {
@@ -69,7 +74,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 // consecutive slots, one atomic per wave (ballot + mbcnt prefix).
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred)
 {
-    uint64_t m = __ballot(pred);
+    uint64_t m = wballot(pred);
     if (m == 0) return 0;
     int leader = __ffsll((unsigned long long)m) - 1;
     uint32_t base = 0;
@@ -305,7 +310,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
     TravRay r;
     TravState ts;
     for (;;) {
-        uint64_t idle = __ballot(!active);
+        uint64_t idle = wballot(!active);
         uint32_t nidle = (uint32_t)__popcll(idle);
         if (nidle >= (uint32_t)REFILL && (res < res_end || !drained)) {
             while (res >= res_end && !drained) {  // renew the reservation (wave-uniform)
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                     const uint32_t cj = counts[lane_id() * kCtr];
                     const uint32_t hj = __hip_atomic_load(&heads[lane_id() * kCtr], __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t open = __ballot(hj < cj);
+                    const uint64_t open = wballot(hj < cj);
                     if (open == 0) {
                         drained = true;
                         break;
@@ -366,7 +371,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
             }
             res += take;
         }
-        if (!__any(active)) {
+        if (!wany(active)) {
             if (res >= res_end && drained) break;
             continue;
         }
@@ -376,8 +381,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                 if (VOTE) {
                     // one step kind per round: inner nodes or leaves, whichever more
                     // lanes are waiting for, so each load issues with more lanes
-                    const uint64_t at_leaf = __ballot(!done && ts.node < 0);
-                    const uint64_t at_node = __ballot(!done && ts.node >= 0);
+                    const uint64_t at_leaf = wballot(!done && ts.node < 0);
+                    const uint64_t at_node = wballot(!done && ts.node >= 0);
                     if (at_leaf == 0 && at_node == 0) break;
                     const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
                     if (!done && (ts.node < 0) == leaf_round) {
@@ -571,15 +576,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
 
     for (;;) {
         const bool wants = has_pix ? !in_query : !exhausted;
-        const uint64_t need = __ballot(wants);
-        const uint64_t trav = __ballot(in_query);
+        const uint64_t need = wballot(wants);
+        const uint64_t trav = wballot(in_query);
         // Sparse waves (TAIL = D > 0): a wave shades once SHADE_MIN lanes wait, or
         // -- when fewer than D*SHADE_MIN lanes still hold a pixel -- once 1/D of
         // them wait, so the last pixels of a wave (the frame's critical path at
         // low load) do not idle until every other lane's query has finished.
         int shade_min = SHADE_MIN;
         if (TAIL > 0) {
-            const int act = __popcll(__ballot(has_pix));
+            const int act = __popcll(wballot(has_pix));
             shade_min = max(1, min(SHADE_MIN, act / TAIL));
         }
         if (need != 0 && (__popcll(need) >= shade_min || trav == 0)) {
@@ -594,7 +599,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             bool cam = false, start = false, sany = false;
             f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
             // ---- new pixels for idle lanes (wave-uniform reservation)
-            const uint64_t nopix = __ballot(!has_pix && !exhausted);
+            const uint64_t nopix = wballot(!has_pix && !exhausted);
             if (nopix != 0) {
                 while (res >= res_end && !exhausted) {
                     const int64_t lo = (int64_t)seg * pc.seg_cap;
@@ -705,13 +710,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             pt_shade += t - pt_t;
             pt_t = t;
         }
-        if (!__any(in_query)) {
-            if (exhausted && !__any(has_pix)) break;
+        if (!wany(in_query)) {
+            if (exhausted && !wany(has_pix)) break;
             continue;
         }
         for (int k = 0; k < STEPS; ++k) {  // traversal rounds
-            const uint64_t at_leaf = __ballot(in_query && ts.node < 0);
-            const uint64_t at_node = __ballot(in_query && ts.node >= 0);
+            const uint64_t at_leaf = wballot(in_query && ts.node < 0);
+            const uint64_t at_node = wballot(in_query && ts.node >= 0);
             if ((at_leaf | at_node) == 0) break;
             const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
             // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds

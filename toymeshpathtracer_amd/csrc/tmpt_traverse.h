@@ -463,7 +463,9 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                                                    TravCount& cnt)
 {
     if (ts.node >= 0) {
-        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
+        // 32-bit byte offset off an SGPR base: one VALU for the address
+        const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
+                                                        ((uint32_t)ts.node << 6));
         const uint4 A = p[0], B = p[1], C = p[2];
         const int4 L = reinterpret_cast<const int4*>(p)[3];
         if (COUNT) ++cnt.nodes;
@@ -541,7 +543,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         const uint32_t first = code & kLeafFirstMask;
         const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
         for (uint32_t k = 0; k < n; ++k) {
-            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
+            const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sv.tri_pre) +
+                                                              (first + k) * (uint32_t)sizeof(TriPre));
             float4 a = p[0], b = p[1], c = p[2];
             if (COUNT) ++cnt.tris;
             float t, u, v;
