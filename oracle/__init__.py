@@ -178,8 +178,9 @@ class Scene:
         t = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
         self.n = t.shape[0]
         if bmin is None:  # main.cpp:296-297,312 octree bounds from the OBJ bounds
-            bmin = t.reshape(-1, 3).min(0)
-            bmax = t.reshape(-1, 3).max(0)
+            v = t.reshape(-1, 3)
+            bmin = v.min(0) if len(v) else np.zeros(3, np.float32)
+            bmax = v.max(0) if len(v) else np.zeros(3, np.float32)
         bmin = np.asarray(bmin, np.float32)
         bmax = np.asarray(bmax, np.float32)
         extra = (bmax - bmin) * np.float32(0.7)

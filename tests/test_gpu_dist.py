@@ -1,0 +1,49 @@
+"""bench.py's N>1 path end to end on the one GPU of the box: two ranks under
+torch.distributed.run share cuda:0 with the gloo backend (the driver's 8-GPU
+run uses nccl = RCCL; the band partition, device tiles, gather, assembly and
+max-over-ranks timing are the same code).  Rank 0's frame must equal the
+single-process frame byte for byte."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+from PIL import Image
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(args, env_extra=None, timeout=600):
+    env = dict(os.environ, **(env_extra or {}))
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_gloo_matches_single(gpu, tmp_path):
+    one = tmp_path / "one.png"
+    two = tmp_path / "two.png"
+    common = ["--config", "teapot720", "--steps", "1", "--warmup", "0", "--no-cpu"]
+    r1 = _bench(["bench.py", "--gpus", "1", "--save", str(one)] + common)
+    port = _free_port()
+    r2 = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                 "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                 "--dist-backend", "gloo", "--save", str(two)] + common)
+    assert r2["n_gpus"] == 2 and r2["scaling"] == "strong"
+    assert r2["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
+    a = np.asarray(Image.open(one).convert("RGBA"))
+    b = np.asarray(Image.open(two).convert("RGBA"))
+    assert np.array_equal(a, b)

@@ -291,3 +291,77 @@ def test_progressive_shards_and_errors(gpu):
     with pytest.raises(tm.TmptError, match="spp_begin"):
         sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=6, spp_count=1)
     sc.close()
+
+
+# ---------------------------------------------------------------- edge cases
+def _oracle_pixel(tris, cam, w, h, spp):
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_LINEAR if len(tris) < 64 else oracle.ACCEL_BVH,
+                       tie=oracle.TIE_INDEX)
+    return osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL)
+
+
+@pytest.mark.parametrize("w,h,spp", [(1, 1, 1), (3, 2, 5), (65, 1, 2), (1, 130, 2), (97, 33, 1)])
+@pytest.mark.parametrize("engine", [tm.ENGINE_PERSISTENT, tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+def test_ragged_image_sizes(gpu, w, h, spp, engine):
+    """Images smaller than a wave, a band or a segment, odd sizes, one row or
+    one column: same pixels and ray count as the oracle."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=engine)
+    ref, rrays = _oracle_pixel(tris, cam, w, h, spp)
+    assert rays == rrays and np.array_equal(img, ref)
+    sc.close()
+
+
+@pytest.mark.parametrize("ntris", [0, 1, 2])
+@pytest.mark.parametrize("engine", [tm.ENGINE_PERSISTENT, tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+def test_tiny_scenes(gpu, ntris, engine):
+    """Scenes of 0, 1 and 2 triangles (no floor): the BVH degenerates to a
+    single leaf or nothing; every query still matches the linear scan."""
+    tris, bmin, bmax = tm.load_scene(data("cube.obj"))
+    sub = np.ascontiguousarray(tris[:ntris])
+    cam = tm.Camera.for_scene(bmin, bmax, 48, 27)
+    with tm.Scene(sub) as sc:
+        img, rays = sc.trace_image(cam, 48, 27, 3, seed_mode=tm.SEED_PIXEL, engine=engine)
+        o = np.tile(cam.as_array()[:3], (64, 1)).astype(np.float32)
+        d = np.random.default_rng(ntris).normal(size=(64, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        ids, _ = sc.hit_scene_batch(np.concatenate([o, d], 1), 0.001, 1e7)
+    ref, rrays = _oracle_pixel(sub, cam, 48, 27, 3)
+    assert rays == rrays and np.array_equal(img, ref)
+    if ntris == 0:
+        assert (ids == -1).all()
+
+
+def test_max_spp_and_sample_count_edges(gpu):
+    """spp at the reference's maximum (1024, main.cpp:258-280) on a tiny image."""
+    tris, bmin, bmax, sc = _scene("cube.obj")
+    cam = tm.Camera.for_scene(bmin, bmax, 8, 4)
+    img, rays = sc.trace_image(cam, 8, 4, 1024, seed_mode=tm.SEED_PIXEL)
+    ref, rrays = _oracle_pixel(tris, cam, 8, 4, 1024)
+    assert rays == rrays and np.array_equal(img, ref)
+    with pytest.raises(tm.TmptError, match="samplesPerPixel"):
+        sc.trace_image(cam, 8, 4, 1025, seed_mode=tm.SEED_PIXEL)
+    sc.close()
+
+
+def test_bench_frame_full_size_shards(gpu, sponza_path):
+    """BASELINE configs[3] at full size (1920x1080x64): the 8 row-band shards
+    reassemble to the single-GPU frame, ray counts add up, run to run identical
+    (size-independent properties of the full workload)."""
+    from toymeshpathtracer_amd import shard
+
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 64
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris) as sc:
+        full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16)
+        again, rays2 = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16)
+        tiles, total = [], 0
+        for k in range(8):
+            t, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16, shard=k, num_shards=8)
+            tiles.append(t)
+            total += r
+    frame = np.zeros_like(full)
+    shard.assemble(tiles, shard.all_rows(h, 16, 8), frame)
+    assert rays == rays2 == total and np.array_equal(full, again) and np.array_equal(full, frame)

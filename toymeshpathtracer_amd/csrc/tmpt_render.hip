@@ -362,9 +362,9 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                     trav_init(ts, kMaxT);
                     ++traced;
                     steps = 0;
-                    if (!ray_has_nan(o, d)) {
+                    if (sv.n > 0 && !ray_has_nan(o, d)) {
                         active = true;
-                    } else if (!ANY) {  // provably no hit (ray_has_nan): a counted miss
+                    } else if (!ANY) {  // provably no hit (NaN ray, empty scene): a counted miss
                         s.hid[p] = -1;
                     }
                 }
@@ -702,7 +702,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 trav_init(ts, kMaxT);
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
-                in_query = !ray_has_nan(so, sd);  // NaN: a counted miss
+                in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
             }
         }
         if (PROF) {
