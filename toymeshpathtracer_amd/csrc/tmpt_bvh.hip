@@ -707,6 +707,28 @@ inline int blocks_for(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 }  // namespace
 
+// LSD radix sort of (key, value) pairs by the low `bits` bits of the key
+// (stable; 8 bits per pass, ping-pong).  hist: 256 * ceil(n / kSortTile)
+// words.  Returns the buffer pair holding the result (0: keys/vals, 1: tmp).
+int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tkeys, uint32_t* tvals, int32_t n,
+                     int bits, uint32_t* hist, hipStream_t st)
+{
+    const int nb = std::max(1, blocks_for(n, kSortTile));
+    uint32_t *ki = keys, *vi = vals, *ko = tkeys, *vo = tvals;
+    int which = 0;
+    for (int shift = 0; shift < bits; shift += 8) {
+        k_sort_hist<<<nb, kBlock, 0, st>>>(ki, n, shift, nb, hist);
+        k_scan_1block<<<1, 1024, 0, st>>>(hist, 256 * nb);
+        k_sort_scatter<<<nb, kBlock, 0, st>>>(ki, vi, ko, vo, n, shift, nb, hist);
+        std::swap(ki, ko);
+        std::swap(vi, vo);
+        which ^= 1;
+    }
+    return which;
+}
+
+size_t radix_sort_hist_words(int32_t n) { return 256 * (size_t)std::max(1, blocks_for(n, kSortTile)); }
+
 int build_lbvh(Scene& s, const float* d_tris9)
 {
     const int32_t n = s.n;

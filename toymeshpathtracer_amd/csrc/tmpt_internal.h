@@ -107,6 +107,7 @@ struct Scene {
     float4* prog = nullptr;
     size_t prog_slots = 0;
     int32_t prog_key[7] = {0, 0, 0, 0, 0, 0, -1};
+    int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
     // statistics of the last render
     double render_ms = 0.0;
     double extend_ms = 0.0;
@@ -132,6 +133,11 @@ const char* last_error();
 
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
+// device radix sort of (key, value) pairs (tmpt_bvh.hip); returns 0 if the
+// result is in (keys, vals), 1 if in (tkeys, tvals)
+int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tkeys, uint32_t* tvals, int32_t n,
+                     int bits, uint32_t* hist, hipStream_t st);
+size_t radix_sort_hist_words(int32_t n);
 // sincos table for the current device (created on first use, never freed)
 const float2* device_sincos_table(int device);
 

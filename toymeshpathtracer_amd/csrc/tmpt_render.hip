@@ -533,11 +533,18 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 //     64-pixel reservation per atomic on segmented heads.
 // No per-bounce grid-wide synchronisation and no path state in HBM: light
 // scalars and the pending bounce ray live in LDS.
+// Pixel supply: the tile's pixel ranks are cut into chunks of kChunk;
+// segment s owns chunks s, s+kSeg, s+2kSeg, ... and its head counts the
+// chunks taken, so all segments together hand out ranks in increasing order
+// (the waves walk segments from their own one, one atomic per chunk).  Rank r
+// is pixel order[r] (a cost-descending order from a pilot pass) or r itself.
 struct PathCtl {
-    uint32_t* heads;  // kSeg pixel-segment heads, stride kCtr
-    uint32_t seg_cap;
+    uint32_t* heads;  // kSeg chunk counters, stride kCtr
+    uint32_t nchunks;
     int64_t P;
-    int cost_map;  // COUNT only: write per-pixel traversal work instead of colour
+    int cost_map;                     // COUNT only: write per-pixel traversal work instead of colour
+    const uint32_t* __restrict__ order;  // rank -> pixel, or null
+    uint32_t* __restrict__ cost_out;     // per-pixel traversal steps of this call, or null
 };
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
@@ -564,6 +571,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     bool has_pix = false, in_query = false, qany = false;
     uint32_t pix = 0, rng = 0, smp = 0, depth = 0;
     uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
+    uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
     // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
     // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
     uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
@@ -602,17 +610,16 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             const uint64_t nopix = wballot(!has_pix && !exhausted);
             if (nopix != 0) {
                 while (res >= res_end && !exhausted) {
-                    const int64_t lo = (int64_t)seg * pc.seg_cap;
-                    const int64_t left = pc.P - lo;
-                    const uint32_t c = left <= 0 ? 0u : (uint32_t)min<int64_t>(left, pc.seg_cap);
+                    // chunks of segment seg: seg, seg + kSeg, ...
+                    const uint32_t c = seg < pc.nchunks ? (pc.nchunks - 1u - seg) / (uint32_t)kSeg + 1u : 0u;
                     uint32_t b = c;
                     if (c != 0) {
-                        if (lane_id() == 0) b = atomicAdd(&pc.heads[seg * kCtr], kChunk);
+                        if (lane_id() == 0) b = atomicAdd(&pc.heads[seg * kCtr], 1u);
                         b = (uint32_t)__shfl((int)b, 0);
                     }
                     if (b < c) {
-                        res = (uint32_t)lo + b;
-                        res_end = (uint32_t)lo + min(b + kChunk, c);
+                        res = (seg + b * (uint32_t)kSeg) * (uint32_t)kChunk;
+                        res_end = (uint32_t)min<int64_t>((int64_t)res + kChunk, pc.P);
                     } else {
                         seg = (seg + 1) & 63u;
                         if (++walked == kSeg) exhausted = true;
@@ -621,7 +628,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const uint32_t take = min((uint32_t)__popcll(nopix), res_end - res);
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
-                    pix = res + k;
+                    pix = pc.order ? pc.order[res + k] : res + k;
+                    psteps = 0;
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
@@ -683,6 +691,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         cam = true;
                     } else {
                         if (a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
+                        if (pc.cost_out) pc.cost_out[pix] = psteps;
                         out[pix] = (COUNT && pc.cost_map)
                                        ? cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris - work0
                                        : pack_pixel(col, a.out_recip);
@@ -736,6 +745,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
                     in_query = false;
                 }
+                if (pc.cost_out) ++psteps;
             }
             if (PROF) {
                 const uint64_t t = stamp();
@@ -771,6 +781,28 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             atomicAdd(&counters[15], (unsigned long long)pt_leaf);
         }
     }
+}
+
+// Pilot ordering: 3x3 box sum of each pixel's pilot-pass traversal steps,
+// as a 16-bit key that sorts ascending = most expensive first.
+__global__ void __launch_bounds__(256) k_order_keys(const uint32_t* __restrict__ cost, int32_t W,
+                                                     int32_t rows, uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ vals)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)W * rows) return;
+    const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+    uint32_t sum = 0;
+    for (int dy = -1; dy <= 1; ++dy) {
+        const int yy = y + dy;
+        if (yy < 0 || yy >= rows) continue;
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = x + dx;
+            if (xx >= 0 && xx < W) sum += cost[(int64_t)yy * W + xx];
+        }
+    }
+    keys[i] = 65535u - min(sum, 65535u);
+    vals[i] = (uint32_t)i;
 }
 
 // ============================================================ host side
@@ -1086,9 +1118,26 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
     }
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const int64_t P = a.slots;
+    // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
+    // a shard has several pixels per resident lane, the frame ends with the
+    // chains of the pixels started last.  A first pass runs kPilot samples of
+    // every pixel and records its traversal steps; the remaining samples run
+    // with pixels handed out most expensive first (3x3-smoothed pilot cost).
+    // The passes continue each pixel's RNG stream and colour sum exactly as
+    // progressive spp does, so the image is the single-pass image bit for bit.
+    // TMPT_PILOT=<samples> (0 = off).
+    // TMPT_PILOT_RATIO: minimum pixels per resident lane for the ordering (x10).
+    int pilot = 4, ratio10 = 0;
+    if (const char* e = getenv("TMPT_PILOT")) pilot = std::max(0, atoi(e));
+    if (const char* e = getenv("TMPT_PILOT_RATIO")) ratio10 = std::max(0, atoi(e));
+    const bool ordered = pilot > 0 && !count && !prof && a.smp_begin == 0 && a.smp_end == a.spp &&
+                         a.spp >= 2 * pilot && 10 * P >= (int64_t)ratio10 * grid * kBlk && P < (1ll << 31);
     const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
-    if (ensure_ws(s, (ovf_words + head_words) * 4)) return -1;
+    const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
+    const size_t extra_words = ordered ? (size_t)P * (4 + 5) + hist_words : 0;
+    if (ensure_ws(s, (ovf_words + head_words + extra_words) * 4)) return -1;
     uint32_t* heads = (uint32_t*)s.ws + ovf_words;
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
     PathCtl pc;
@@ -1097,10 +1146,42 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const char* cm = getenv("TMPT_COST_MAP");
     pc.cost_map = count && cm && atoi(cm) != 0;
     pc.heads = heads;
-    pc.P = a.slots;
-    pc.seg_cap = (uint32_t)std::max<int64_t>(1, (a.slots + kSeg - 1) / kSeg);
-    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, pc, d_out, (uint32_t*)s.ws, d_counters);
+    pc.P = P;
+    pc.nchunks = (uint32_t)((P + kChunk - 1) / kChunk);
+    pc.order = nullptr;
+    pc.cost_out = nullptr;
+    if (!ordered) {
+        fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, pc, d_out, (uint32_t*)s.ws, d_counters);
+        TMPT_HIP(hipGetLastError());
+        s.path_launches = 1;
+        return 0;
+    }
+    uint32_t* base = heads + head_words;
+    float4* state = reinterpret_cast<float4*>(base);  // P x {colour sum, rng}
+    uint32_t* cost = base + 4 * (size_t)P;
+    uint32_t* keys = cost + P;
+    uint32_t* vals = keys + P;
+    uint32_t* tkeys = vals + P;
+    uint32_t* tvals = tkeys + P;
+    uint32_t* hist = tvals + P;
+    RenderArgs a1 = a;  // pass 1: samples [0, pilot), per-pixel steps
+    a1.smp_end = pilot;
+    a1.out_recip = 1.0f / (float)pilot;
+    a1.prog = state;
+    pc.cost_out = cost;
+    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a1, pc, d_out, (uint32_t*)s.ws, d_counters);
     TMPT_HIP(hipGetLastError());
+    k_order_keys<<<(unsigned)((P + 255) / 256), 256, 0, s.stream>>>(cost, a.W, a.tile_rows, keys, vals);
+    const int which = radix_sort_pairs(keys, vals, tkeys, tvals, (int32_t)P, 16, hist, s.stream);
+    TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
+    RenderArgs a2 = a;  // pass 2: samples [pilot, spp), most expensive pixels first
+    a2.smp_begin = pilot;
+    a2.prog = state;
+    pc.cost_out = nullptr;
+    pc.order = which ? tvals : vals;
+    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a2, pc, d_out, (uint32_t*)s.ws, d_counters);
+    TMPT_HIP(hipGetLastError());
+    s.path_launches = 2;
     return 0;
 }
 
@@ -1204,7 +1285,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.tri_tests = c[2];
         s.shadow_node_visits = c[4];
         s.shadow_tri_tests = c[5];
-        s.extend_launches = 1;
+        s.extend_launches = s.path_launches;  // same k_path instantiation per launch
         s.iterations = 1;
         if (c[13] + c[14] + c[15]) {
             const double tot = (double)(c[13] + c[14] + c[15]);
