@@ -656,17 +656,33 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
                         f3 pos, nrm;
                         hit_record(sv, ts.best, ts.bu, ts.bv, pos, nrm);
-                        light[depth * BLOCK] = light_cosine(nrm, r.d);  // zeroed if occluded
+                        const float lc = light_cosine(nrm, r.d);
+                        light[depth * BLOCK] = lc;  // zeroed if occluded
                         f3 rnd = random_unit_vector(rng, sv.sincos);
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
-                        nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
-                        nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
                         ++depth;
-                        start = true;  // shadow query toward the light
-                        sany = true;
-                        so = pos;
-                        sd = ldir;
+                        if (lc > 0.0f) {
+                            nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
+                            nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
+                            start = true;  // shadow query toward the light
+                            sany = true;
+                            so = pos;
+                            sd = ldir;
+                        } else {
+                            // The reference still calls HitScene for the shadow ray
+                            // (main.cpp:57, counted), but a surface turned away from
+                            // the light adds max(0, cos) = 0 whatever it answers
+                            // (main.cpp:59-67): count the query, skip the traversal.
+                            ++rays_s;
+                            if (depth < (uint32_t)kMaxDepth) {
+                                start = true;  // the scattered ray of this bounce
+                                so = pos;
+                                sd = nd;
+                            } else {
+                                finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
+                            }
+                        }
                     } else {
                         color = sky(r.d);  // main.cpp:106-107
                         finish = true;
@@ -1112,8 +1128,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, 1, T_>            \
                    : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, 1, T_>  \
                                : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 3, 1, T_>);
-            TMPT_PV(16, 16, 1, 0) TMPT_PV(8, 8, 1, 1) TMPT_PV(8, 8, 1, 2) TMPT_PV(8, 8, 1, 4) TMPT_PV(8, 8, 2, 2)
-            TMPT_PV(16, 16, 1, 2) TMPT_PV(16, 16, 1, 4)
+            TMPT_PV(8, 8, 0, 2) TMPT_PV(8, 8, 2, 2) TMPT_PV(4, 8, 1, 2) TMPT_PV(4, 4, 1, 2)
+            TMPT_PV(16, 16, 1, 2) TMPT_PV(8, 4, 1, 2)
 #undef TMPT_PV
         }
     }
