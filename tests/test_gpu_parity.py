@@ -236,6 +236,7 @@ def test_count_visits_instrumentation(gpu):
     seen = {}
     for engine, node in ((tm.ENGINE_WAVEFRONT, "q"), (tm.ENGINE_PERSISTENT, "q"), (tm.ENGINE_PERSISTENT, "f")):
         os.environ["TMPT_NODE"] = node
+        os.environ["TMPT_SHADOW_GRID"] = "0"  # BVH shadow queries in both engines
         try:
             img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine,
                                        count_visits=True)
@@ -243,6 +244,7 @@ def test_count_visits_instrumentation(gpu):
             img2, _ = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, engine=engine)
         finally:
             del os.environ["TMPT_NODE"]
+            del os.environ["TMPT_SHADOW_GRID"]
         assert st.extend_rays + st.shadow_rays == rays
         assert st.node_visits > st.extend_rays and st.tri_tests > 0 and st.shadow_node_visits > 0
         assert np.array_equal(img, img2)
@@ -253,6 +255,17 @@ def test_count_visits_instrumentation(gpu):
     # BVH4F (unquantised boxes) culls at least as tightly, same image
     c = seen[(tm.ENGINE_PERSISTENT, "f")]
     assert np.array_equal(a[0], c[0]) and c[1] == a[1] and c[2] <= a[2] and c[3] <= a[3]
+    sc.close()
+    # shadow queries through the light-space grid: no node visits, only triangle tests
+    os.environ["TMPT_SHADOW_GRID"] = "256"
+    try:
+        sc = tm.Scene(tris)
+    finally:
+        del os.environ["TMPT_SHADOW_GRID"]
+    img, rays = sc.trace_image(cam, 160, 90, 2, seed_mode=tm.SEED_PIXEL, count_visits=True)
+    st = sc.stats()
+    assert np.array_equal(img, a[0]) and st.extend_rays + st.shadow_rays == rays
+    assert st.shadow_node_visits == 0 and st.shadow_tri_tests > 0
     sc.close()
 
 
@@ -365,3 +378,56 @@ def test_bench_frame_full_size_shards(gpu, sponza_path):
     frame = np.zeros_like(full)
     shard.assemble(tiles, shard.all_rows(h, 16, 8), frame)
     assert rays == rays2 == total and np.array_equal(full, again) and np.array_equal(full, frame)
+
+
+# ---------------------------------------------------------------- shadow grid
+def _light_dir_f32():
+    """kLightDir = normalize(-0.7, 1, 0.5) (main.cpp:36) in GLM's float order."""
+    v = np.array([-0.7, 1.0, 0.5], np.float32)
+    d = np.float32(np.float32(v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
+    return (v * np.float32(np.float32(1.0) / np.sqrt(d))).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["cube.obj", "suzanne.obj", "teapot.obj", "sponza"])
+def test_shadow_grid_matches_exact_query(gpu, sponza_path, name):
+    """Shadow rays (direction = the light's) through the light-space grid give
+    the exact query's hit/miss: from surface points (the shadow rays the
+    renderer casts, incl. self-intersection at t < kMinT), from vertices and
+    edge midpoints, and from random points."""
+    path = sponza_path if name == "sponza" else data(name)
+    tris, bmin, bmax = tm.load_scene(path)
+    os.environ["TMPT_SHADOW_GRID"] = "1024"  # build the grid (off by default)
+    try:
+        sc = tm.Scene(tris)
+    finally:
+        del os.environ["TMPT_SHADOW_GRID"]
+    L = _light_dir_f32()
+    rng = np.random.default_rng(5)
+    prim = _random_rays(tris, 60_000, seed=13)
+    pids, phits = sc.hit_scene_batch(prim, 0.001, 1.0e7)
+    surf = phits[pids >= 0, :3]
+    v = tris.reshape(-1, 3)
+    edges = ((tris[:, [0, 1, 2]] + tris[:, [1, 2, 0]]) * np.float32(0.5)).reshape(-1, 3)
+    lo, hi = v.min(0), v.max(0)
+    rnd = (lo + rng.random((20_000, 3)) * (hi - lo)).astype(np.float32)
+    o = np.concatenate([surf, v[:40_000], edges[:40_000], rnd]).astype(np.float32)
+    rays = np.concatenate([o, np.broadcast_to(L, o.shape)], 1).astype(np.float32)
+    gids, _ = sc.hit_scene_batch(rays, 0.001, 1.0e7, any_hit=True)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX)
+    oids, _ = osc.hit_batch(rays, 0.001, 1.0e7)
+    bad = np.nonzero((gids >= 0) != (oids >= 0))[0]
+    assert bad.size == 0, f"{bad.size} shadow mismatches of {len(rays)}, first {bad[:5]}"
+    assert (oids >= 0).sum() > 100 and (oids < 0).sum() > 100
+    sc.close()
+
+
+def test_shadow_grid_frame_equals_bvh_shadows(gpu, monkeypatch):
+    """Whole frames with the grid and with BVH shadow queries: same bytes, same rays."""
+    monkeypatch.setenv("TMPT_SHADOW_GRID", "1024")
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    cam = tm.Camera.for_scene(bmin, bmax, 320, 180)
+    a, ra = sc.trace_image(cam, 320, 180, 8, seed_mode=tm.SEED_PIXEL)
+    monkeypatch.setenv("TMPT_SHADOW_GRID", "0")
+    b, rb = sc.trace_image(cam, 320, 180, 8, seed_mode=tm.SEED_PIXEL)
+    assert ra == rb and np.array_equal(a, b)
+    sc.close()

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <new>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -140,6 +141,12 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
     int rc = build_lbvh(s, d_tris);
     if (d_tris) (void)hipFree(d_tris);
     if (rc) return fail(rc);
+    {
+        auto t0 = std::chrono::steady_clock::now();
+        rc = build_shadow_grid(s, tris);
+        if (rc) return fail(rc);
+        s.build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     *out = h;
     return 0;
     TMPT_GUARD_END
@@ -155,6 +162,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.nodes4f) (void)hipFree(s.nodes4f);
     if (s.prog) (void)hipFree(s.prog);
+    free_shadow_grid(s);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);

@@ -60,6 +60,24 @@ constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
 
+// Light-space grid for the shadow query (tmpt_shadow.hip): R x R cells over
+// the plane orthogonal to the light direction, per cell the triangles whose
+// projection overlaps it, sorted by how far up the light direction they reach.
+struct ShadowGrid {
+    float U[3] = {0, 0, 0}, V[3] = {0, 0, 0};  // plane axes (L = light_dir())
+    float u0 = 0, v0 = 0, inv_cu = 0, inv_cv = 0;
+    int R = 0;                  // 0: no grid
+    uint32_t* start = nullptr;  // R*R + 1 entry offsets, cell = iv * R + iu
+    float* tmax = nullptr;      // per entry: max over the triangle's vertices of dot(v, L), rounded up
+    uint32_t* slot = nullptr;   // per entry: tri_pre slot
+    int64_t n_entries = 0;
+    // the path kernel's form: each entry's TriPre copied into tri_pre after the
+    // scene's slots (from index base), so a cell's list is one contiguous range
+    // that the traversal's leaf step tests like any leaf
+    uint2* cell = nullptr;      // per cell: {first tri_pre index, count}
+    int32_t base = 0;
+};
+
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x
     float4 b;  // e1.yz, e2.xy
@@ -95,6 +113,7 @@ struct Scene {
     int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
     bool has_bvh2 = true;  // the LBVH2 (A/B layout) matches tri_pre only for the LBVH builder
     TriPre* tri_pre = nullptr;
+    ShadowGrid sgrid;  // shadow-query grid (tmpt_shadow.hip), R = 0 if none
     TriOrig* tri_orig = nullptr;
     const float2* sincos = nullptr;  // borrowed from the per-device table
     hipStream_t stream = nullptr;
@@ -138,6 +157,9 @@ int build_lbvh(Scene& s, const float* d_tris9);
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tkeys, uint32_t* tvals, int32_t n,
                      int bits, uint32_t* hist, hipStream_t st);
 size_t radix_sort_hist_words(int32_t n);
+// shadow-query grid (tmpt_shadow.hip); host_tris = the n x 9 input floats
+int build_shadow_grid(Scene& s, const float* host_tris);
+void free_shadow_grid(Scene& s);
 // sincos table for the current device (created on first use, never freed)
 const float2* device_sincos_table(int device);
 

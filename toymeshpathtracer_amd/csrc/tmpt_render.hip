@@ -116,11 +116,15 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
-            ++rays;  // shadow ray, main.cpp:57-59
-            float ts, us, vs;
-            int sid = traverse<WIDE, true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT, ts,
-                                            us, vs, st, cnt);
-            lbuf[depth * BLOCK] = sid >= 0 ? 0.0f : light_cosine(nrm, d);
+            ++rays;  // shadow ray, main.cpp:57-59 (always counted)
+            float lc = light_cosine(nrm, d);
+            if (lc > 0.0f) {  // a zero light term does not depend on the answer
+                float ts, us, vs;
+                int sid = traverse<WIDE, true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT,
+                                                      ts, us, vs, st, cnt);
+                if (sid >= 0) lc = 0.0f;
+            }
+            lbuf[depth * BLOCK] = lc;
             f3 rnd = random_unit_vector(rng, sv.sincos);  // main.cpp:71-72
             f3 target = pos + nrm + rnd;
             d = normalize(target - pos);
@@ -198,7 +202,13 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         const float* r = rays + 6 * i;
         f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
         float t, u, v;
-        int id = traverse<WIDE, ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
+        const f3 ld = light_dir();
+        int id;
+        if (ANY && sv.sg.R > 0 && tmin == kMinT && tmax == kMaxT && d.x == ld.x && d.y == ld.y &&
+            d.z == ld.z && !ray_has_nan(o, d) && sv.n > 0)
+            id = shadow_grid_hit(sv, o, d, t, u, v);  // the shadow query's own structure
+        else
+            id = traverse<WIDE, ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
         ids[i] = id;
         if (id >= 0) {
             f3 pos, nrm;
@@ -606,6 +616,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             // branches, so the wave runs each at most once per round.
             bool cam = false, start = false, sany = false;
             f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
+            uint2 gcell = make_uint2(0u, 0u);  // shadow-grid leaf range of this round's shadow query
             // ---- new pixels for idle lanes (wave-uniform reservation)
             const uint64_t nopix = wballot(!has_pix && !exhausted);
             if (nopix != 0) {
@@ -662,14 +673,23 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
+                        bool traced = false;
                         if (lc > 0.0f) {
-                            nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
-                            nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
-                            start = true;  // shadow query toward the light
-                            sany = true;
-                            so = pos;
-                            sd = ldir;
-                        } else {
+                            // shadow query: with the light-space grid, the triangles of
+                            // the origin's cell (one leaf range, tested by the leaf
+                            // steps of the traversal rounds); without, the BVH
+                            if (sv.sg.R > 0) gcell = shadow_grid_cell(sv, pos);
+                            if (sv.sg.R == 0 || gcell.y != 0) {
+                                nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
+                                nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
+                                start = true;  // shadow query toward the light
+                                sany = true;
+                                so = pos;
+                                sd = ldir;
+                                traced = true;
+                            }
+                        }
+                        if (!traced) {  // nothing to trace (no light term, or an empty cell)
                             // The reference still calls HitScene for the shadow ray
                             // (main.cpp:57, counted), but a surface turned away from
                             // the light adds max(0, cos) = 0 whatever it answers
@@ -728,6 +748,14 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
+                if (gcell.y != 0) {  // grid shadow query: its cell's list as chunks of leaf ranges
+                    const uint32_t n0 = min(gcell.y, (uint32_t)kLeafMaxTris);
+                    for (uint32_t f = gcell.x + n0; f < gcell.x + gcell.y; f += kLeafMaxTris)
+                        st.push(ts.sp, (int)(0x80000000u |
+                                             ((min((uint32_t)kLeafMaxTris, gcell.x + gcell.y - f) - 1u)
+                                              << kLeafCountShift) | f));
+                    ts.node = (int)(0x80000000u | ((n0 - 1u) << kLeafCountShift) | gcell.x);
+                }
             }
         }
         if (PROF) {
@@ -852,8 +880,11 @@ int ensure_ws(Scene& s, size_t bytes)
 
 SceneView view(const Scene& s)
 {
-    return SceneView{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
-                     s.tri_orig, s.sincos, s.n};
+    SceneView v{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
+                s.tri_orig, s.sincos, s.n, s.sgrid};
+    const char* e = getenv("TMPT_SHADOW_GRID");  // 0: keep the grid out of the queries (A/B)
+    if (e && atoi(e) == 0) v.sg.R = 0;
+    return v;
 }
 
 RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)

@@ -106,6 +106,7 @@ struct SceneView {
     const TriOrig* __restrict__ tri_orig;
     const float2* __restrict__ sincos;
     int32_t n;
+    ShadowGrid sg;  // by value: axes, origin, scale, device arrays (R = 0: none)
 };
 
 struct TravCount {
@@ -598,6 +599,54 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
 {
     return __builtin_isnan(o.x) | __builtin_isnan(o.y) | __builtin_isnan(o.z) | __builtin_isnan(d.x) |
            __builtin_isnan(d.y) | __builtin_isnan(d.z);
+}
+
+// Shadow query through the light-space grid (tmpt_shadow.hip): is some
+// triangle hit by (p, light_dir()) with t in [kMinT, kMaxT]?  One cell, a
+// binary search past the triangles that end below p along L, then the
+// bit-exact Moller-Trumbore test in order until one accepts.  Returns the
+// original triangle index of that hit or -1 (t, u, v of the hit).
+__device__ __forceinline__ int shadow_grid_hit(const SceneView& sv, f3 p, f3 ldir, float& t, float& u,
+                                               float& v)
+{
+    const ShadowGrid& g = sv.sg;
+    const float pu = p.x * g.U[0] + p.y * g.U[1] + p.z * g.U[2];
+    const float pv = p.x * g.V[0] + p.y * g.V[1] + p.z * g.V[2];
+    const float fu = (pu - g.u0) * g.inv_cu, fv = (pv - g.v0) * g.inv_cv;
+    // outside the padded projection of every triangle (or NaN): nothing to hit
+    if (!(fu >= 0.0f && fu < (float)g.R && fv >= 0.0f && fv < (float)g.R)) return -1;
+    const uint32_t c = (uint32_t)(int)fv * (uint32_t)g.R + (uint32_t)(int)fu;
+    uint32_t lo = g.start[c];
+    const uint32_t end = g.start[c + 1];
+    // a hit at t >= kMinT reaches dot(p, L) + kMinT up L; the margin covers
+    // float rounding of dot(p, L) and of Moller-Trumbore's t
+    const float dl = p.x * ldir.x + p.y * ldir.y + p.z * ldir.z;
+    const float thr = dl + kMinT - 1e-4f * (1.0f + fabsf(dl));
+    uint32_t hi = end;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (g.tmax[m] < thr) lo = m + 1;
+        else hi = m;
+    }
+    for (uint32_t k = lo; k < end; ++k) {
+        const float4* q = reinterpret_cast<const float4*>(sv.tri_pre + g.slot[k]);
+        const float4 a = q[0], b = q[1], cc = q[2];
+        if (mt_test(p, ldir, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, cc.x), kMinT, kMaxT, t, u, v))
+            return __float_as_int(cc.y);
+    }
+    return -1;
+}
+
+// The shadow-grid cell of a shadow ray's origin as a tri_pre range
+// {first, count} (count 0: no triangle can be hit).
+__device__ __forceinline__ uint2 shadow_grid_cell(const SceneView& sv, f3 p)
+{
+    const ShadowGrid& g = sv.sg;
+    const float pu = p.x * g.U[0] + p.y * g.U[1] + p.z * g.U[2];
+    const float pv = p.x * g.V[0] + p.y * g.V[1] + p.z * g.V[2];
+    const float fu = (pu - g.u0) * g.inv_cu, fv = (pv - g.v0) * g.inv_cv;
+    if (!(fu >= 0.0f && fu < (float)g.R && fv >= 0.0f && fv < (float)g.R)) return make_uint2(0u, 0u);
+    return g.cell[(uint32_t)(int)fv * (uint32_t)g.R + (uint32_t)(int)fu];
 }
 
 // Whole query in one call.  Returns the original triangle index or -1.
