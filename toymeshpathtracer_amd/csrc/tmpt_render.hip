@@ -587,6 +587,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
     // PROF: wave-uniform s_memtime cycles in shading rounds, node rounds, leaf rounds
     uint64_t pt_shade = 0, pt_node = 0, pt_leaf = 0, pt_t = PROF ? stamp() : 0;
+    // PROF >= 2: the shading round split (pixel fetch, hit/finish shading, camera, query set-up)
+    uint64_t ps_fetch = 0, ps_shade = 0, ps_cam = 0, ps_start = 0;
     f3 col = mk(0.0f, 0.0f, 0.0f);
     TravRay r;
     TravState ts;
@@ -658,6 +660,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     cam = true;
                 }
                 res += take;
+            }
+            uint64_t ps_t = 0;
+            if (PROF >= 2) {
+                ps_t = stamp();
+                ps_fetch += ps_t - pt_t;
             }
             // ---- finished queries: shade
             if (has_pix && !in_query && !cam) {
@@ -735,12 +742,22 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     }
                 }
             }
+            if (PROF >= 2) {
+                const uint64_t t = stamp();
+                ps_shade += t - ps_t;
+                ps_t = t;
+            }
             if (cam) {  // next camera sample of this lane's pixel (main.cpp:212-216)
                 const int lr = (int)(pix / (uint32_t)a.W);
                 const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
                 camera_sample(a.cam, (uint32_t)x, (uint32_t)tile_row_to_y(a, lr), a.invW, a.invH, rng,
                               so, sd);
                 start = true;
+            }
+            if (PROF >= 2) {
+                const uint64_t t = stamp();
+                ps_cam += t - ps_t;
+                ps_t = t;
             }
             if (start) {
                 r = make_trav_ray(so, sd);
@@ -757,6 +774,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     ts.node = (int)(0x80000000u | ((n0 - 1u) << kLeafCountShift) | gcell.x);
                 }
             }
+            if (PROF >= 2) ps_start += stamp() - ps_t;
         }
         if (PROF) {
             const uint64_t t = stamp();
@@ -823,6 +841,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             atomicAdd(&counters[13], (unsigned long long)pt_shade);
             atomicAdd(&counters[14], (unsigned long long)pt_node);
             atomicAdd(&counters[15], (unsigned long long)pt_leaf);
+        }
+        if (PROF >= 2) {
+            atomicAdd(&counters[16], (unsigned long long)ps_fetch);
+            atomicAdd(&counters[17], (unsigned long long)ps_shade);
+            atomicAdd(&counters[18], (unsigned long long)ps_cam);
+            atomicAdd(&counters[19], (unsigned long long)ps_start);
         }
     }
 }
@@ -1149,7 +1173,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
     const char* pe = getenv("TMPT_PROF");
     const bool prof = pe && atoi(pe) != 0 && !count && fmt == 3;
-    if (prof) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 1>;
+    if (prof) fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 2>
+                                 : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 1>;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
         int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
@@ -1281,7 +1306,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.prog_key[6] = -1;  // valid again only once this pass completes
     }
     unsigned long long* d_counters = nullptr;
-    constexpr int kCounters = 16;
+    constexpr int kCounters = 24;
     TMPT_HIP(hipMallocAsync((void**)&d_counters, kCounters * sizeof(unsigned long long), s.stream));
     TMPT_HIP(hipMemsetAsync(d_counters, 0, kCounters * sizeof(unsigned long long), s.stream));
     hipEvent_t e0, e1;
@@ -1339,6 +1364,10 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
             fprintf(stderr, "k_path wave time: shading %.1f%%, node rounds %.1f%%, leaf rounds %.1f%% "
                             "(%.3g wave-cycles)\n",
                     100.0 * c[13] / tot, 100.0 * c[14] / tot, 100.0 * c[15] / tot, tot);
+            if (c[16] + c[17] + c[18] + c[19])
+                fprintf(stderr, "  shading split: ballots+pixel fetch %.1f%%, shade/finish %.1f%%, camera %.1f%%, "
+                                "query set-up %.1f%% (of all wave time)\n",
+                        100.0 * c[16] / tot, 100.0 * c[17] / tot, 100.0 * c[18] / tot, 100.0 * c[19] / tot);
         }
         if (count && getenv("TMPT_ROUND_LOG"))  // diagnostic: wave-round efficiency
             fprintf(stderr,
