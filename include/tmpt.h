@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 2  /* 2: progressive spp (tmpt_render_desc.spp_begin / spp_count) */
+#define TMPT_ABI_VERSION 3  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -129,6 +129,18 @@ int tmpt_scene_hit(const tmpt_scene* scene, const float* rays, int64_t n, float 
  * *ray_count = every HitScene call (main.cpp:57,91), counted in uint64. */
 int tmpt_render(tmpt_scene* scene, const tmpt_camera* cam, const tmpt_render_desc* desc,
                 uint8_t* rgba_out, uint64_t* ray_count);
+/* main.cpp:312-331 over several devices in ONE process (SURVEY.md §8e's
+ * single-process form): a scene per entry of devices[] (created here, freed on
+ * return; a device may repeat), the frame's 16-row bands dealt round-robin to
+ * them, one host thread per device, the tiles assembled into rgba_full
+ * (width*height*4, row 0 = bottom, as tmpt_render).  desc's band_rows, shard,
+ * num_shards and flags are taken over; *seconds = wall time of the renders
+ * (scene builds excluded, main.cpp:319-333); *ray_count = all devices' rays.
+ * The one-process-per-GPU form is bench.py (torch.distributed + RCCL). */
+int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, const tmpt_render_desc* desc,
+                      const int32_t* devices, int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count,
+                      double* seconds);
+
 /* rows in the tile of desc's shard; global row of tile row r */
 int32_t tmpt_tile_rows(const tmpt_render_desc* desc);
 int32_t tmpt_tile_row_to_y(const tmpt_render_desc* desc, int32_t r);

@@ -431,3 +431,20 @@ def test_shadow_grid_frame_equals_bvh_shadows(gpu, monkeypatch):
     b, rb = sc.trace_image(cam, 320, 180, 8, seed_mode=tm.SEED_PIXEL)
     assert ra == rb and np.array_equal(a, b)
     sc.close()
+
+
+# ---------------------------------------------------------------- single-process multi-device
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_render_multi_equals_single_device(gpu, devices):
+    """tmpt_render_multi (SURVEY §8e single-process form): bands dealt to one
+    scene per listed device (here the one GPU, repeated), one host thread each,
+    assembled frame == the single-call frame, rays add up."""
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    w, h, spp = 320, 200, 4
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    ref, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    img, mrays, secs = tm.render_multi(tris, cam, w, h, spp, devices)
+    assert mrays == rays and np.array_equal(img, ref) and secs > 0
+    with pytest.raises(tm.TmptError, match="device"):
+        tm.render_multi(tris, cam, w, h, spp, [0, 99])
+    sc.close()

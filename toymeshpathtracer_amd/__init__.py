@@ -29,7 +29,7 @@ import numpy as np
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
     "SEED_ROW", "SEED_PIXEL", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
-    "tile_rows", "tile_row_to_y",
+    "tile_rows", "tile_row_to_y", "render_multi",
 ]
 
 SEED_ROW, SEED_PIXEL = 0, 1
@@ -120,6 +120,10 @@ _scene_hit = _sig("tmpt_scene_hit", ctypes.c_int, [ctypes.c_void_p, _f32p, ctype
                                                    _f32p, _i32p])
 _render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Camera),
                                              ctypes.POINTER(_Desc), ctypes.c_void_p, _u64p])
+_render_multi = _sig("tmpt_render_multi", ctypes.c_int,
+                     [_f32p, ctypes.c_int32, ctypes.POINTER(_Camera), ctypes.POINTER(_Desc),
+                      ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.c_void_p, _u64p,
+                      ctypes.POINTER(ctypes.c_double)])
 _tile_rows = _sig("tmpt_tile_rows", ctypes.c_int32, [ctypes.POINTER(_Desc)])
 _tile_row_to_y = _sig("tmpt_tile_row_to_y", ctypes.c_int32, [ctypes.POINTER(_Desc), ctypes.c_int32])
 _stats = _sig("tmpt_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Stats)])
@@ -130,7 +134,7 @@ _abi = _sig("tmpt_abi_version", ctypes.c_int, [])
 #: every symbol include/tmpt.h declares (checked by tests/test_abi.py)
 EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_scene",
            "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_destroy", "tmpt_scene_hit",
-           "tmpt_render", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
+           "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
            "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version")
 
 
@@ -367,6 +371,23 @@ class Scene:
         s = _Stats()
         _check(_stats(self._h, ctypes.byref(s)), "stats")
         return RenderStats(*[getattr(s, f) for f, _ in _Stats._fields_])
+
+
+def render_multi(tris: np.ndarray, camera: "Camera", width: int, height: int, spp: int, devices,
+                 seed_mode: int = SEED_PIXEL, engine: int = ENGINE_PERSISTENT) -> Tuple[np.ndarray, int, float]:
+    """One frame over several devices in this process (tmpt_render_multi):
+    returns (rgba[height, width, 4], rays, render seconds).  A device may repeat."""
+    t = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    devs = (ctypes.c_int32 * len(devices))(*devices)
+    img = np.zeros((height, width, 4), np.uint8)
+    rays = ctypes.c_uint64()
+    secs = ctypes.c_double()
+    d = _desc(width, height, spp, seed_mode, 0, 0, 1, engine)
+    cam = camera._to_c()
+    _check(_render_multi(t.ctypes.data_as(_f32p), t.shape[0], ctypes.byref(cam), ctypes.byref(d), devs,
+                         len(devices), img.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays),
+                         ctypes.byref(secs)), "render_multi")
+    return img, int(rays.value), float(secs.value)
 
 
 def write_png(path: str, rgba: np.ndarray) -> None:

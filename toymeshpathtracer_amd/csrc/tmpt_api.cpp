@@ -7,6 +7,7 @@
 #include <new>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tmpt.h"
@@ -263,6 +264,79 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     }
     if (!dev_out && d_out) (void)hipFree(d_out);
     return rc;
+    TMPT_GUARD_END
+}
+
+int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, const tmpt_render_desc* desc,
+                      const int32_t* devices, int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count,
+                      double* seconds)
+{
+    TMPT_GUARD_BEGIN
+    if (!cam || !desc || !devices || ndevices < 1 || !rgba_full || (n > 0 && !tris))
+        return bad("tmpt_render_multi: bad arguments");
+    const int nd = ndevices;
+    std::vector<tmpt_scene*> scenes((size_t)nd, nullptr);
+    std::vector<int> rcs((size_t)nd, 0);
+    std::vector<std::string> errs((size_t)nd);
+    auto destroy_all = [&]() {
+        for (auto* sc : scenes) tmpt_scene_destroy(sc);
+    };
+    {  // scene per device, concurrently (error text is thread-local: keep each thread's)
+        std::vector<std::thread> th;
+        for (int g = 0; g < nd; ++g)
+            th.emplace_back([&, g]() {
+                rcs[(size_t)g] = tmpt_scene_create(tris, n, devices[g], &scenes[(size_t)g]);
+                if (rcs[(size_t)g]) errs[(size_t)g] = tmpt_last_error();
+            });
+        for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < nd; ++g)
+        if (rcs[(size_t)g]) {
+            destroy_all();
+            return (set_error("tmpt_render_multi: " + errs[(size_t)g]), rcs[(size_t)g]);
+        }
+    std::vector<tmpt_render_desc> ds((size_t)nd, *desc);
+    std::vector<std::vector<uint8_t>> tiles((size_t)nd);
+    std::vector<uint64_t> rays((size_t)nd, 0);
+    for (int g = 0; g < nd; ++g) {
+        tmpt_render_desc& d = ds[(size_t)g];
+        d.band_rows = nd > 1 ? 16 : desc->band_rows;
+        d.shard = g;
+        d.num_shards = nd;
+        d.flags = 0;
+        tiles[(size_t)g].resize((size_t)std::max(0, tmpt_tile_rows(&d)) * (size_t)std::max(0, d.width) * 4);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        std::vector<std::thread> th;
+        for (int g = 0; g < nd; ++g)
+            th.emplace_back([&, g]() {
+                rcs[(size_t)g] = tmpt_render(scenes[(size_t)g], cam, &ds[(size_t)g], tiles[(size_t)g].data(),
+                                             &rays[(size_t)g]);
+                if (rcs[(size_t)g]) errs[(size_t)g] = tmpt_last_error();
+            });
+        for (auto& t : th) t.join();
+    }
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    uint64_t total = 0;
+    for (int g = 0; g < nd; ++g) {
+        if (rcs[(size_t)g]) {
+            destroy_all();
+            return (set_error("tmpt_render_multi: " + errs[(size_t)g]), rcs[(size_t)g]);
+        }
+        total += rays[(size_t)g];
+        const tmpt_render_desc& d = ds[(size_t)g];
+        const int rows = tmpt_tile_rows(&d);
+        for (int r = 0; r < rows; ++r) {
+            const int y = tmpt_tile_row_to_y(&d, r);
+            memcpy(rgba_full + (size_t)y * d.width * 4, tiles[(size_t)g].data() + (size_t)r * d.width * 4,
+                   (size_t)d.width * 4);
+        }
+    }
+    destroy_all();
+    if (ray_count) *ray_count = total;
+    if (seconds) *seconds = dt;
+    return 0;
     TMPT_GUARD_END
 }
 

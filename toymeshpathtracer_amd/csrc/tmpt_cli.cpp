@@ -11,7 +11,6 @@
 
 #include <chrono>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "tmpt.h"
@@ -65,52 +64,24 @@ int main(int argc, const char** argv)
     tmpt_camera cam;
     tmpt_camera_for_scene(&cam, bmin, bmax, w, h, strstr(obj, "sponza.obj") != nullptr);
 
-    std::vector<tmpt_scene*> scenes(gpus, nullptr);
-    std::vector<int> rcs(gpus, 0);
-    double t0 = now_s();
-    {
-        std::vector<std::thread> th;
-        for (int g = 0; g < gpus; ++g)
-            th.emplace_back([&, g]() { rcs[g] = tmpt_scene_create(tris, n, device + g, &scenes[g]); });
-        for (auto& t : th) t.join();
-    }
-    for (int g = 0; g < gpus; ++g)
-        if (rcs[g]) { printf("ERROR: scene init failed: %s\n", tmpt_last_error()); return 1; }
-    printf("Initialized scene '%s' (%i tris) in %.3fs\n", obj, n, now_s() - t0);
-
     std::vector<uint8_t> image((size_t)w * h * 4, 0);
-    std::vector<std::vector<uint8_t>> tiles(gpus);
-    std::vector<uint64_t> rays(gpus, 0);
-    std::vector<tmpt_render_desc> desc(gpus);
-    for (int g = 0; g < gpus; ++g) {
-        memset(&desc[g], 0, sizeof(tmpt_render_desc));
-        desc[g].width = w; desc[g].height = h; desc[g].spp = spp; desc[g].seed_mode = seed;
-        desc[g].band_rows = gpus > 1 ? 16 : 0; desc[g].shard = g; desc[g].num_shards = gpus;
-        desc[g].engine = engine;
-        tiles[g].resize((size_t)tmpt_tile_rows(&desc[g]) * w * 4);
-    }
-    t0 = now_s();
-    {
-        std::vector<std::thread> th;
-        for (int g = 0; g < gpus; ++g)
-            th.emplace_back([&, g]() { rcs[g] = tmpt_render(scenes[g], &cam, &desc[g], tiles[g].data(), &rays[g]); });
-        for (auto& t : th) t.join();
-    }
-    const double dt = now_s() - t0;
+    tmpt_render_desc desc;
+    memset(&desc, 0, sizeof(desc));
+    desc.width = w; desc.height = h; desc.spp = spp; desc.seed_mode = seed; desc.engine = engine;
+    std::vector<int32_t> devs(gpus);
+    for (int g = 0; g < gpus; ++g) devs[g] = device + g;
     uint64_t total = 0;
-    for (int g = 0; g < gpus; ++g) {
-        if (rcs[g]) { printf("ERROR: render failed: %s\n", tmpt_last_error()); return 1; }
-        total += rays[g];
-        int rows = tmpt_tile_rows(&desc[g]);
-        for (int r = 0; r < rows; ++r) {
-            int y = tmpt_tile_row_to_y(&desc[g], r);
-            memcpy(&image[(size_t)y * w * 4], &tiles[g][(size_t)r * w * 4], (size_t)w * 4);
-        }
+    double dt = 0.0;
+    const double t0 = now_s();
+    // scene builds + renders; tmpt_render_multi times the renders alone (main.cpp:319-333)
+    if (tmpt_render_multi(tris, n, &cam, &desc, devs.data(), gpus, image.data(), &total, &dt)) {
+        printf("ERROR: %s\n", tmpt_last_error());
+        return 1;
     }
+    printf("Initialized scene '%s' (%i tris) in %.3fs\n", obj, n, now_s() - t0 - dt);
     printf("Rendered scene at %ix%i,%ispp in %.3f s\n", w, h, spp, dt);
     printf("- %.1f K Rays, %.1f K Rays/s\n", total / 1000.0, total / 1000.0 / dt);
     if (tmpt_write_png(out, image.data(), w, h)) { printf("ERROR: %s\n", tmpt_last_error()); return 1; }
-    for (auto* s : scenes) tmpt_scene_destroy(s);
     tmpt_free(tris);
     return 0;
 }
