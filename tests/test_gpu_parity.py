@@ -448,3 +448,24 @@ def test_render_multi_equals_single_device(gpu, devices):
     with pytest.raises(tm.TmptError, match="device"):
         tm.render_multi(tris, cam, w, h, spp, [0, 99])
     sc.close()
+
+
+# ---------------------------------------------------------------- the drop-in CLI
+@pytest.mark.parametrize("name", ["cube", "teapot"])
+def test_cli_reproduces_reference_binary(gpu, tmp_path, name):
+    """`tmpt 640 360 4 <obj>` (the reference's command line, row seeding by
+    default) writes the PNG whose pixels hash to the reference binary's
+    (SURVEY §8c pins, the same as test_oracle's) and logs its ray count."""
+    import subprocess
+    from PIL import Image
+
+    cli = os.path.join(os.path.dirname(tm.lib_path), "tmpt")
+    out = tmp_path / "o.png"
+    r = subprocess.run([cli, "640", "360", "4", data(name + ".obj"), "--out", str(out)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    img = np.asarray(Image.open(out).convert("RGBA"))  # top-down as written
+    sha = hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]
+    want_sha, want_krays = REFERENCE_BINARY[name]
+    assert sha == want_sha
+    assert f"- {want_krays:.1f} K Rays" in r.stdout
