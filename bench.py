@@ -6,7 +6,7 @@ is launched by torch.distributed.run, one rank per GPU.  One *step* = one full
 frame of BASELINE.json configs[3]: sponza.obj 1920x1080, 64 spp (the
 deterministic stand-in scene, data/gen_standin_sponza.py; the real sponza.obj
 is absent from the reference), pixel-mode seeding, persistent path engine.  The frame
-is sharded over the N GPUs in 16-row bands dealt round-robin (total work fixed:
+is sharded over the N GPUs in rows dealt round-robin (1-row bands; total work fixed:
 strong scaling); each rank renders its bands straight into a device tensor and
 one RCCL gather over xGMI assembles the image on rank 0 -- inside the timed
 region.  value = all rays of all ranks / max-over-ranks wall time.
@@ -44,7 +44,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "MRays/s on sponza.obj 1920x1080 64spp at 1/2/4/8 GPUs; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
-BAND_ROWS = 16
+BAND_ROWS = 1   # rows dealt round-robin: every rank gets H/N rows of statistically equal cost
 S_NODE = 64            # bytes per visited node: BVH4Q (4 quantised child boxes + links) or BVH2
 S_TRI = 36             # bytes per triangle test (3 x vec3), SURVEY.md §8d
 S_RAY = 32 + 16        # ray read + hit write, SURVEY.md §8d

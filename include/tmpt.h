@@ -131,7 +131,7 @@ int tmpt_render(tmpt_scene* scene, const tmpt_camera* cam, const tmpt_render_des
                 uint8_t* rgba_out, uint64_t* ray_count);
 /* main.cpp:312-331 over several devices in ONE process (SURVEY.md §8e's
  * single-process form): a scene per entry of devices[] (created here, freed on
- * return; a device may repeat), the frame's 16-row bands dealt round-robin to
+ * return; a device may repeat), the frame's rows dealt round-robin to
  * them, one host thread per device, the tiles assembled into rgba_full
  * (width*height*4, row 0 = bottom, as tmpt_render).  desc's band_rows, shard,
  * num_shards and flags are taken over; *seconds = wall time of the renders

@@ -29,6 +29,7 @@ spp = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 scene_name = os.environ.get("TUNE_SCENE", "sponza")
 SHARDS = int(os.environ.get("TUNE_SHARDS", "1"))  # >1: render shard 0 of N (per-rank load at N GPUs)
+BAND = int(os.environ.get("TUNE_BAND", "16"))  # rows per band dealt round-robin to the shards
 W, H = 1920, 1080
 path = gen_standin_sponza.ensure() if scene_name == "sponza" else os.path.join(ROOT, "data", scene_name)
 tris, bmin, bmax = tm.load_scene(path)
@@ -72,7 +73,7 @@ for r in range(rounds):
             if env.get(k) is not None:
                 os.environ[k] = env[k]
         t0 = time.perf_counter()
-        img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_PIXEL, band_rows=16, shard=0,
+        img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_PIXEL, band_rows=BAND, shard=0,
                                    num_shards=SHARDS, engine=ENGINES[env.get("ENGINE", "persistent")])
         dt = time.perf_counter() - t0
         st = sc.stats()

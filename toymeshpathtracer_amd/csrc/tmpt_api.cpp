@@ -300,7 +300,7 @@ int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, cons
     std::vector<uint64_t> rays((size_t)nd, 0);
     for (int g = 0; g < nd; ++g) {
         tmpt_render_desc& d = ds[(size_t)g];
-        d.band_rows = nd > 1 ? 16 : desc->band_rows;
+        d.band_rows = nd > 1 ? 1 : desc->band_rows;  // rows dealt round-robin: balanced shards
         d.shard = g;
         d.num_shards = nd;
         d.flags = 0;
