@@ -21,7 +21,7 @@ import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
 BUILD_KEYS = ("TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
-RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID")
+RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]

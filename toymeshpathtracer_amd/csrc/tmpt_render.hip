@@ -555,7 +555,12 @@ struct PathCtl {
     int cost_map;                     // COUNT only: write per-pixel traversal work instead of colour
     const uint32_t* __restrict__ order;  // rank -> pixel, or null
     uint32_t* __restrict__ cost_out;     // per-pixel traversal steps of this call, or null
+    uint32_t prio_q;  // ordered pass: ranks per wave-priority level (s_setprio 3..0), 0 = off
+    uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
+    uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
 };
+
+constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per block (7.5 KB)
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
           int OCC = 1, int TAIL = 0, int PROF = 0>
@@ -571,6 +576,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     float* light = &s_light[threadIdx.x];
     float* nxt = &s_next[threadIdx.x];
+    if (FMT == 4) {  // the top BVH4 levels (nodes are numbered level by level) in LDS
+        __shared__ uint4 s_top[kTopNodes * 4];
+        const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
+        const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
+        for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
+        __syncthreads();
+        st.top = (const lds_u4*)s_top;
+        st.ntop = ntop;
+    }
     TravCount cnt, cnt_s;  // COUNT: closest-hit and shadow queries apart
     uint32_t rays_e = 0, rays_s = 0;
     const f3 ldir = light_dir();
@@ -631,14 +645,23 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         b = (uint32_t)__shfl((int)b, 0);
                     }
                     if (b < c) {
-                        res = (seg + b * (uint32_t)kSeg) * (uint32_t)kChunk;
-                        res_end = (uint32_t)min<int64_t>((int64_t)res + kChunk, pc.P);
+                        res = (seg + b * (uint32_t)kSeg) * pc.chunk;
+                        res_end = (uint32_t)min<int64_t>((int64_t)res + pc.chunk, pc.P);
+                        if (pc.prio_q != 0) {  // issue priority by cost rank (wave-uniform)
+                            const uint32_t q = res / pc.prio_q;
+                            if (q == 0) __builtin_amdgcn_s_setprio(3);
+                            else if (q == 1) __builtin_amdgcn_s_setprio(2);
+                            else if (q == 2) __builtin_amdgcn_s_setprio(1);
+                            else __builtin_amdgcn_s_setprio(0);
+                        }
                     } else {
                         seg = (seg + 1) & 63u;
                         if (++walked == kSeg) exhausted = true;
                     }
                 }
-                const uint32_t take = min((uint32_t)__popcll(nopix), res_end - res);
+                uint32_t take = min((uint32_t)__popcll(nopix), res_end - res);
+                if (pc.lane_cap < 64u)  // low load: pixels spread over all resident waves
+                    take = min(take, pc.lane_cap - min(pc.lane_cap, (uint32_t)__popcll(wballot(has_pix))));
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
                     pix = pc.order ? pc.order[res + k] : res + k;
@@ -905,7 +928,7 @@ int ensure_ws(Scene& s, size_t bytes)
 SceneView view(const Scene& s)
 {
     SceneView v{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
-                s.tri_orig, s.sincos, s.n, s.sgrid};
+                s.tri_orig, s.sincos, s.n, s.sgrid, s.n_nodes4};
     const char* e = getenv("TMPT_SHADOW_GRID");  // 0: keep the grid out of the queries (A/B)
     if (e && atoi(e) == 0) v.sg.R = 0;
     return v;
@@ -1155,37 +1178,40 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
 {
-    constexpr int kPathSL = 16, kPathSteps = 8, kShadeMin = 8;
+    // traversal rounds between shading checks / lanes waiting that trigger a
+    // shading round (A/B on the bench frame at 1 and 8 shards, tools/tune.py)
+    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16;
     // node step (TMPT_NODE, A/B): q = BVH4Q min/max decode, f = BVH4F f32 boxes,
-    // s = BVH4Q octant decode + full near-to-far sort, default = octant decode,
-    // nearest child first (others pairwise ordered)
+    // s = BVH4Q octant decode + full near-to-far sort, n = octant decode,
+    // nearest child first (others pairwise ordered), default = n with the top
+    // kTopNodes nodes read from a per-block LDS copy
     const char* nf = getenv("TMPT_NODE");
-    const int fmt = nf && nf[0] == 'q' ? 0 : (nf && nf[0] == 'f' ? 1 : (nf && nf[0] == 's' ? 2 : 3));
-    constexpr int kSparse = 2;  // sparse-wave shading threshold divisor (k_path TAIL)
+    const char nc = nf ? nf[0] : 't';
+    const int fmt = nc == 'q' ? 0 : (nc == 'f' ? 1 : (nc == 's' ? 2 : (nc == 'n' ? 3 : 4)));
+    constexpr int kSparse = 4;  // sparse-wave shading threshold divisor (k_path TAIL)
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
     PathFn fn = nullptr;
 #define TMPT_PF(C_, F_) \
     if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 1, kSparse>;
-    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3)
-    TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3)
+    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3) TMPT_PF(true, 4)
+    TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3) TMPT_PF(false, 4)
 #undef TMPT_PF
-    const bool quant = fmt == 0;
     // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
     const char* pe = getenv("TMPT_PROF");
-    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 3;
-    if (prof) fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 2>
-                                 : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 3, 1, kSparse, 1>;
+    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 4;
+    if (prof) fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2>
+                                 : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1>;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
         int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
         if (sscanf(tune, "%d,%d,%d,%d,%d", &a0, &a1, &a2, &a3, &a4) >= 4 && a0 == 900 && !count) {
 #define TMPT_PV(ST_, SM_, V_, T_)                                                  \
     if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == T_)                           \
-        fn = quant ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 0, 1, T_>            \
-                   : (fmt == 1 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 1, 1, T_>  \
-                               : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 3, 1, T_>);
-            TMPT_PV(8, 8, 0, 2) TMPT_PV(8, 8, 2, 2) TMPT_PV(4, 8, 1, 2) TMPT_PV(4, 4, 1, 2)
-            TMPT_PV(16, 16, 1, 2) TMPT_PV(8, 4, 1, 2)
+        fn = fmt == 4 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 4, 1, T_>           \
+                      : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 3, 1, T_>;
+            TMPT_PV(8, 8, 1, 2) TMPT_PV(8, 8, 2, 2) TMPT_PV(16, 16, 1, 2) TMPT_PV(16, 16, 2, 4)
+            TMPT_PV(32, 32, 1, 4) TMPT_PV(16, 8, 1, 2) TMPT_PV(16, 8, 1, 4) TMPT_PV(12, 12, 1, 4)
+            TMPT_PV(20, 16, 1, 4)
 #undef TMPT_PV
         }
     }
@@ -1219,9 +1245,24 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.cost_map = count && cm && atoi(cm) != 0;
     pc.heads = heads;
     pc.P = P;
-    pc.nchunks = (uint32_t)((P + kChunk - 1) / kChunk);
+
     pc.order = nullptr;
     pc.cost_out = nullptr;
+    pc.prio_q = 0;
+    // Small shards (at most a quarter as many pixels as resident lanes): a wave
+    // holds at most 32 pixels at once, so the pixels spread over more SIMD
+    // slots and each wave's chain -- the frame's critical path at that load --
+    // has fewer lanes to interleave (bench frame, 1/32 shard: 44.1 -> 40.9 ms;
+    // at 1/16 (half the lanes) it measured 44.4 -> 45.5 ms, so not there; 16
+    // lanes per wave was slower still).  TMPT_WAVE_CAP=<c> fixes the cap (64 = off).
+    {
+        const int64_t waves = std::max<int64_t>(1, (int64_t)grid * (kBlk / 64));
+        int64_t c = P <= waves * 16 ? 32 : 64;
+        if (const char* e = getenv("TMPT_WAVE_CAP")) c = atoi(e);
+        pc.lane_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(64, c));
+    }
+    pc.chunk = std::min<uint32_t>(kChunk, pc.lane_cap);
+    pc.nchunks = (uint32_t)((P + pc.chunk - 1) / pc.chunk);
     if (!ordered) {
         fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, pc, d_out, (uint32_t*)s.ws, d_counters);
         TMPT_HIP(hipGetLastError());
@@ -1251,6 +1292,12 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     a2.prog = state;
     pc.cost_out = nullptr;
     pc.order = which ? tvals : vals;
+    // TMPT_PRIO=<d>: waves holding ranks of the first d-th of the order issue at
+    // priority 3, the next d-th at 2, the next at 1 (0 = off)
+    if (const char* e = getenv("TMPT_PRIO")) {
+        const int d = atoi(e);
+        if (d > 0) pc.prio_q = (uint32_t)std::max<int64_t>(1, (P + d - 1) / d);
+    }
     fn<<<grid, kBlk, 0, s.stream>>>(view(s), a2, pc, d_out, (uint32_t*)s.ws, d_counters);
     TMPT_HIP(hipGetLastError());
     s.path_launches = 2;

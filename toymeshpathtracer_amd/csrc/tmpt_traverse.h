@@ -70,6 +70,8 @@ __device__ __forceinline__ bool slab(const TravRay& r, float lx, float ly, float
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
 // Per-lane traversal stack: the top SL entries in LDS ([depth][lane], a wave's
 // access to one depth hits 64 banks), deeper ones in a per-lane global area.
@@ -81,12 +83,33 @@ template <int BLOCK, int SL>
 struct TravStack {
     lds_u32* lds;    // &s_stack[threadIdx.x]; entry k at lds[k * BLOCK]
     uint32_t* glob;  // kStackTotal - SL entries of this lane
+    const lds_u4* top = nullptr;  // LDS copy of BVH4 nodes [0, ntop) (FMT 4), 4 uint4 each
+    uint32_t ntop = 0;
     __device__ __forceinline__ TravStack(uint32_t* l, uint32_t* g) : lds((lds_u32*)l), glob(g) {}
     __device__ __forceinline__ void push(int& sp, int v)
     {
         if (SL >= kStackTotal || sp < SL) lds[sp * BLOCK] = (uint32_t)v;
         else glob[sp - SL] = (uint32_t)v;
         ++sp;
+    }
+    // Up to three pushes (c0 first, c2 last = popped first), branch-free while
+    // the LDS part has room for three: the valid ones are compacted into
+    // consecutive slots by selects and all three slots are written (slots
+    // above the new depth are free, so the extra writes are harmless).
+    __device__ __forceinline__ void push3(int& sp, bool v0, int c0, bool v1, int c1, bool v2, int c2)
+    {
+        if (sp + 3 <= SL) {
+            const int s0 = v0 ? c0 : (v1 ? c1 : c2);
+            const int s1 = (v0 && v1) ? c1 : c2;
+            lds[sp * BLOCK] = (uint32_t)s0;
+            lds[(sp + 1) * BLOCK] = (uint32_t)s1;
+            lds[(sp + 2) * BLOCK] = (uint32_t)c2;
+            sp += (int)v0 + (int)v1 + (int)v2;
+        } else {
+            if (v0) push(sp, c0);
+            if (v1) push(sp, c1);
+            if (v2) push(sp, c2);
+        }
     }
     __device__ __forceinline__ int pop(int& sp)
     {
@@ -107,6 +130,7 @@ struct SceneView {
     const float2* __restrict__ sincos;
     int32_t n;
     ShadowGrid sg;  // by value: axes, origin, scale, device arrays (R = 0: none)
+    int32_t n_nodes4 = 0;
 };
 
 struct TravCount {
@@ -458,17 +482,28 @@ __device__ __forceinline__ bool trav_step4f_mixed(const SceneView& sv, const Tra
 // child pairs, no per-child min/max and no mask test (empty slots carry an
 // inverted box and link to the null leaf).  4 loads per node (the TA cost of a
 // divergent gather scales with bytes per lane) at ~BVH4F's VALU count.
-template <bool COUNT, int BLOCK, int SL, int SORTK = 0>
+template <bool COUNT, int BLOCK, int SL, int SORTK = 0, bool TOPC = false>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt)
 {
     if (ts.node >= 0) {
         // 32-bit byte offset off an SGPR base: one VALU for the address
-        const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
-                                                        ((uint32_t)ts.node << 6));
-        const uint4 A = p[0], B = p[1], C = p[2];
-        const int4 L = reinterpret_cast<const int4*>(p)[3];
+        uint4 A, B, C;
+        int4 L;
+        if (TOPC && (uint32_t)ts.node < st.ntop) {  // top levels: the block's LDS copy
+            const lds_u4* q = st.top + ((uint32_t)ts.node << 2);
+            const u32x4 a4 = q[0], b4 = q[1], c4 = q[2], l4 = q[3];
+            A = make_uint4(a4.x, a4.y, a4.z, a4.w);
+            B = make_uint4(b4.x, b4.y, b4.z, b4.w);
+            C = make_uint4(c4.x, c4.y, c4.z, c4.w);
+            L = make_int4((int)l4.x, (int)l4.y, (int)l4.z, (int)l4.w);
+        } else {
+            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
+                                                            ((uint32_t)ts.node << 6));
+            A = p[0], B = p[1], C = p[2];
+            L = reinterpret_cast<const int4*>(p)[3];
+        }
         if (COUNT) ++cnt.nodes;
         const float sx = exp_scale(A.w) * r.ix, sy = exp_scale(A.w >> 8) * r.iy,
                     sz = exp_scale(A.w >> 16) * r.iz;
@@ -532,9 +567,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             const float kn = sab ? kb : ka, kno = sab ? ka : kb;
             const int cn = sab ? cb : ca, cno = sab ? ca : cb;
             if (kn != INFINITY) {
-                if (kbo != INFINITY) st.push(ts.sp, cbo);
-                if (kao != INFINITY) st.push(ts.sp, cao);
-                if (kno != INFINITY) st.push(ts.sp, cno);
+                st.push3(ts.sp, kbo != INFINITY, cbo, kao != INFINITY, cao, kno != INFINITY, cno);
                 ts.node = cn;
                 return false;
             }
@@ -576,6 +609,7 @@ __device__ __forceinline__ bool trav_step_fmt(const SceneView& sv, const TravRay
     if (FMT == 1) return trav_step4f_mixed<COUNT>(sv, r, any, ts, st, cnt);
     if (FMT == 2) return trav_step4q2_mixed<COUNT, BLOCK, SL, 0>(sv, r, any, ts, st, cnt);
     if (FMT == 3) return trav_step4q2_mixed<COUNT, BLOCK, SL, 1>(sv, r, any, ts, st, cnt);
+    if (FMT == 4) return trav_step4q2_mixed<COUNT, BLOCK, SL, 1, true>(sv, r, any, ts, st, cnt);
     return trav_step4_mixed<COUNT>(sv, r, any, ts, st, cnt);
 }
 
