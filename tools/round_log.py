@@ -19,7 +19,7 @@ sc = tm.Scene(tris)
 os.environ["TMPT_ROUND_LOG"] = "1"
 for n in shards:
     img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_PERSISTENT,
-                               band_rows=16, shard=0, num_shards=n, count_visits=True)
+                               band_rows=1, shard=0, num_shards=n, count_visits=True)
     st = sc.stats()
     print(f"shards {n}: rays {rays} nodes {st.node_visits + st.shadow_node_visits} "
           f"tris {st.tri_tests + st.shadow_tri_tests} render {st.render_ms:.1f} ms", flush=True)

@@ -1192,7 +1192,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
     PathFn fn = nullptr;
 #define TMPT_PF(C_, F_) \
-    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 1, kSparse>;
+    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 4, kSparse>;
     TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3) TMPT_PF(true, 4)
     TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3) TMPT_PF(false, 4)
 #undef TMPT_PF

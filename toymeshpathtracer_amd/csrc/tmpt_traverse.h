@@ -69,6 +69,15 @@ __device__ __forceinline__ bool slab(const TravRay& r, float lx, float ly, float
     return tn <= tf * kTfarSlack;
 }
 
+// Pins a loaded triangle record's used words in registers at this point (no
+// instruction emitted), so the compiler cannot sink their loads into the
+// branches that consume them.
+__device__ __forceinline__ void materialize(float4& a, float4& b, float4& c)
+{
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(b.x), "+v"(b.y), "+v"(b.z),
+                 "+v"(b.w), "+v"(c.x), "+v"(c.y));
+}
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
@@ -491,18 +500,18 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         // 32-bit byte offset off an SGPR base: one VALU for the address
         uint4 A, B, C;
         int4 L;
-        if (TOPC && (uint32_t)ts.node < st.ntop) {  // top levels: the block's LDS copy
+        if (!TOPC || (uint32_t)ts.node >= st.ntop) {
+            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
+                                                            ((uint32_t)ts.node << 6));
+            A = p[0], B = p[1], C = p[2];
+            L = reinterpret_cast<const int4*>(p)[3];
+        } else {  // top levels: the block's LDS copy
             const lds_u4* q = st.top + ((uint32_t)ts.node << 2);
             const u32x4 a4 = q[0], b4 = q[1], c4 = q[2], l4 = q[3];
             A = make_uint4(a4.x, a4.y, a4.z, a4.w);
             B = make_uint4(b4.x, b4.y, b4.z, b4.w);
             C = make_uint4(c4.x, c4.y, c4.z, c4.w);
             L = make_int4((int)l4.x, (int)l4.y, (int)l4.z, (int)l4.w);
-        } else {
-            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
-                                                            ((uint32_t)ts.node << 6));
-            A = p[0], B = p[1], C = p[2];
-            L = reinterpret_cast<const int4*>(p)[3];
         }
         if (COUNT) ++cnt.nodes;
         const float sx = exp_scale(A.w) * r.ix, sy = exp_scale(A.w >> 8) * r.iy,
@@ -576,10 +585,9 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         const uint32_t code = (uint32_t)ts.node;
         const uint32_t first = code & kLeafFirstMask;
         const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
-        for (uint32_t k = 0; k < n; ++k) {
-            const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sv.tri_pre) +
-                                                              (first + k) * (uint32_t)sizeof(TriPre));
-            float4 a = p[0], b = p[1], c = p[2];
+        const char* base = reinterpret_cast<const char*>(sv.tri_pre);
+        // Accepts (t, u, v, id) by the closest-hit order; true = any-hit query done.
+        auto tri = [&](const float4& a, const float4& b, const float4& c) -> bool {
             if (COUNT) ++cnt.tris;
             float t, u, v;
             if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
@@ -593,6 +601,24 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                     if (any) return true;
                 }
             }
+            return false;
+        };
+        // Both triangles of a (typical) 2-triangle leaf are loaded at once, all
+        // 40 B each, before any test: left alone the compiler sinks the vertex
+        // load behind the determinant test and the second triangle's loads
+        // behind the first's, three dependent memory latencies per leaf step.
+        const float4* p0 = reinterpret_cast<const float4*>(base + first * (uint32_t)sizeof(TriPre));
+        const float4* p1 = reinterpret_cast<const float4*>(base + (first + (n > 1u ? 1u : 0u)) *
+                                                                       (uint32_t)sizeof(TriPre));
+        float4 a0 = p0[0], b0 = p0[1], c0 = p0[2];
+        float4 a1 = p1[0], b1 = p1[1], c1 = p1[2];
+        materialize(a0, b0, c0);
+        materialize(a1, b1, c1);
+        if (tri(a0, b0, c0)) return true;
+        if (n > 1u && tri(a1, b1, c1)) return true;
+        for (uint32_t k = 2; k < n; ++k) {
+            const float4* p = reinterpret_cast<const float4*>(base + (first + k) * (uint32_t)sizeof(TriPre));
+            if (tri(p[0], p[1], p[2])) return true;
         }
     }
     if (ts.sp == 0) return true;
