@@ -380,6 +380,45 @@ def test_bench_frame_full_size_shards(gpu, sponza_path):
     assert rays == rays2 == total and np.array_equal(full, again) and np.array_equal(full, frame)
 
 
+@pytest.mark.parametrize("env", [{}, {"TMPT_HELP": "0"}, {"TMPT_HELP": "1", "TMPT_PAIR": "0"},
+                                 {"TMPT_HELP": "1", "TMPT_PAIR": "40", "TMPT_WAVE_CAP": "48"},
+                                 {"TMPT_HELP": "1", "TMPT_PILOT": "0"}])
+def test_shadow_offload_matches_oracle(gpu, monkeypatch, env):
+    """Low-load shadow offload (k_path HELP: idle lanes trace other lanes' shadow
+    queries; pending light slots; paired expensive/cheap chunks).  A small frame
+    is far below one pixel per resident lane, so the default already offloads;
+    every variant must give the oracle's image and ray count."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    w, h, spp = 320, 180, 16
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_PERSISTENT)
+    sc.close()
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL)
+    assert rays == ref_rays
+    diff = np.nonzero((img != ref).any(-1))
+    assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+
+
+def test_shadow_offload_bench_frame_shard(gpu, monkeypatch, sponza_path):
+    """The bench frame's 1/8 and 1/4 shards (where the offload is on by default)
+    equal the same shards rendered with it forced off, bit for bit."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 64
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris) as sc:
+        for n in (8, 4):
+            monkeypatch.delenv("TMPT_HELP", raising=False)
+            a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=n - 1,
+                                   num_shards=n)
+            monkeypatch.setenv("TMPT_HELP", "0")
+            b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=n - 1,
+                                   num_shards=n)
+            assert ra == rb and np.array_equal(a, b)
+
+
 # ---------------------------------------------------------------- shadow grid
 def _light_dir_f32():
     """kLightDir = normalize(-0.7, 1, 0.5) (main.cpp:36) in GLM's float order."""

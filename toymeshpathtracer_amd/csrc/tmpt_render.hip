@@ -558,12 +558,13 @@ struct PathCtl {
     uint32_t prio_q;  // ordered pass: ranks per wave-priority level (s_setprio 3..0), 0 = off
     uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
     uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
+    uint32_t* __restrict__ tlog;  // PROF: per pixel {start, end (s_memrealtime), steps, shading rounds}
 };
 
 constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per block (7.5 KB)
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
-          int OCC = 1, int TAIL = 0, int PROF = 0>
+          int OCC = 1, int TAIL = 0, int PROF = 0, int HELP = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -576,9 +577,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     float* light = &s_light[threadIdx.x];
     float* nxt = &s_next[threadIdx.x];
+    // HELP: lane ids of this round's offloading lanes, by rank (per wave)
+    __shared__ uint8_t s_pair[HELP ? BLOCK : 1];
     if (FMT == 4) {  // the top BVH4 levels (nodes are numbered level by level) in LDS
-        __shared__ uint4 s_top[kTopNodes * 4];
-        const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
+        // HELP: 4 nodes fewer, so s_pair keeps the block at 4 per CU
+        constexpr int kTop = HELP ? kTopNodes - 4 : kTopNodes;
+        __shared__ uint4 s_top[kTop * 4];
+        const uint32_t ntop = (uint32_t)min(kTop, sv.n_nodes4);
         const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
         for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
         __syncthreads();
@@ -593,9 +598,21 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint32_t res = 0, res_end = 0;
     bool exhausted = pc.P == 0;
     bool has_pix = false, in_query = false, qany = false;
+    // HELP (shadow offload to idle lanes): once the pixel supply is exhausted, a
+    // lane without a pixel becomes a helper that traces another lane's shadow
+    // query (Scatter's HitScene toward the light only gates that bounce's light
+    // term, main.cpp:57-67: it feeds neither the RNG stream nor the path), so
+    // the owner's chain goes on with the scattered ray at once.  The owner's
+    // light slot holds -cosine while the answer is pending (the cosine is > 0
+    // whenever a shadow query is traced); the helper writes 0 (occluded) or
+    // the cosine.  A path whose slots are still pending waits (`waiting`)
+    // before its backward recurrence.
+    bool helper = false, waiting = false;
+    uint32_t hown = 0;  // helper: owner lane << 4 | light slot
     uint32_t pix = 0, rng = 0, smp = 0, depth = 0;
     uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
     uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
+    uint32_t pt0 = 0, pnsh = 0;  // PROF + tlog: pixel start time, shading rounds while held
     // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
     // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
     uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
@@ -609,7 +626,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     trav_init(ts, kMaxT);
 
     for (;;) {
-        const bool wants = has_pix ? !in_query : !exhausted;
+        const bool wants = has_pix ? !in_query : (HELP && helper ? !in_query : !exhausted);
         const uint64_t need = wballot(wants);
         const uint64_t trav = wballot(in_query);
         // Sparse waves (TAIL = D > 0): a wave shades once SHADE_MIN lanes wait, or
@@ -622,7 +639,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             shade_min = max(1, min(SHADE_MIN, act / TAIL));
         }
         if (need != 0 && (__popcll(need) >= shade_min || trav == 0)) {
-            if (COUNT) {
+            if (PROF && has_pix) ++pnsh;
+            if (COUNT || PROF >= 3) {
                 ++rs_sr;
                 rs_sl += (uint64_t)__popcll(need);
                 rs_st += (uint64_t)__popcll(trav);
@@ -634,7 +652,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
             uint2 gcell = make_uint2(0u, 0u);  // shadow-grid leaf range of this round's shadow query
             // ---- new pixels for idle lanes (wave-uniform reservation)
-            const uint64_t nopix = wballot(!has_pix && !exhausted);
+            const uint64_t nopix = wballot(!has_pix && !(HELP && helper) && !exhausted);
             if (nopix != 0) {
                 while (res >= res_end && !exhausted) {
                     // chunks of segment seg: seg, seg + kSeg, ...
@@ -666,6 +684,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
                     pix = pc.order ? pc.order[res + k] : res + k;
                     psteps = 0;
+                    if (PROF && pc.tlog) {
+                        pt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        pnsh = 0;
+                    }
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
@@ -679,21 +701,32 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     }
                     smp = (uint32_t)a.smp_begin;
                     depth = 0;
-                    if (COUNT) work0 = cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
+                    if (COUNT) work0 = pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
+                                                        : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
                     cam = true;
                 }
                 res += take;
             }
+            if (HELP && helper && !in_query) {  // deliver a finished offloaded shadow query
+                float* ol = &s_light[(threadIdx.x & ~63u) + (hown >> 4) + (hown & 15u) * BLOCK];
+                const float v = *ol;
+                *ol = ts.best >= 0 ? 0.0f : -v;
+                helper = false;
+            }
+            if (HELP) __atomic_signal_fence(__ATOMIC_SEQ_CST);
             uint64_t ps_t = 0;
             if (PROF >= 2) {
                 ps_t = stamp();
                 ps_fetch += ps_t - pt_t;
             }
             // ---- finished queries: shade
+            bool finish = false, want_off = false;
+            f3 color = mk(0.0f, 0.0f, 0.0f);
             if (has_pix && !in_query && !cam) {
-                bool finish = false;
-                f3 color = mk(0.0f, 0.0f, 0.0f);
-                if (!qany) {  // closest hit (Trace, main.cpp:91-109)
+                if (HELP && waiting) {  // path ended, shadow answers were pending
+                    finish = true;
+                    if (depth < (uint32_t)kMaxDepth) color = sky(r.d);
+                } else if (!qany) {  // closest hit (Trace, main.cpp:91-109)
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
                         f3 pos, nrm;
                         hit_record(sv, ts.best, ts.bu, ts.bv, pos, nrm);
@@ -717,6 +750,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                                 so = pos;
                                 sd = ldir;
                                 traced = true;
+                                want_off = HELP != 0 && sv.sg.R == 0;
                             }
                         }
                         if (!traced) {  // nothing to trace (no light term, or an empty cell)
@@ -747,7 +781,48 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
                     }
                 }
-                if (finish) {
+            }
+            if (HELP) {  // pair lanes starting a shadow query with idle lanes
+                const uint64_t S = wballot(want_off);
+                // lanes left without a pixel after this round's fetch (supply
+                // exhausted, or the wave's pixel cap reached) are free to help
+                const uint64_t I = S ? wballot(!has_pix && !helper && !in_query) : 0ull;
+                if (I != 0) {
+                    const uint32_t n = min(__popcll(S), __popcll(I));
+                    const uint32_t ks = (uint32_t)__popcll(S & lt), ki = (uint32_t)__popcll(I & lt);
+                    const uint32_t wb = threadIdx.x & ~63u;
+                    if (want_off && ks < n) s_pair[wb + ks] = (uint8_t)lane_id();
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    const bool idle = ((I >> lane_id()) & 1ull) != 0 && ki < n;
+                    const int src = idle ? (int)s_pair[wb + ki] : (int)lane_id();
+                    const float hx = __shfl(so.x, src), hy = __shfl(so.y, src), hz = __shfl(so.z, src);
+                    const uint32_t hs = (uint32_t)__shfl((int)depth, src) - 1u;
+                    if (want_off && ks < n) {  // offloaded: go on with the scattered ray
+                        light[(depth - 1) * BLOCK] = -light[(depth - 1) * BLOCK];
+                        sany = false;
+                        if (depth < (uint32_t)kMaxDepth) {
+                            sd = mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]);
+                        } else {
+                            start = false;
+                            finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
+                        }
+                    }
+                    if (idle) {
+                        helper = true;
+                        hown = ((uint32_t)src << 4) | hs;
+                        start = true;
+                        sany = true;
+                        so = mk(hx, hy, hz);
+                        sd = ldir;
+                    }
+                }
+            }
+            if (finish) {
+                bool pend = false;
+                if (HELP)
+                    for (int kk = 0; kk < (int)depth; ++kk) pend |= light[kk * BLOCK] < 0.0f;
+                waiting = pend;
+                if (!pend) {
                     for (int kk = (int)depth - 1; kk >= 0; --kk)
                         color = backward_step(color, light[kk * BLOCK]);
                     col = col + color;
@@ -758,8 +833,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     } else {
                         if (a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
                         if (pc.cost_out) pc.cost_out[pix] = psteps;
+                        if (PROF && pc.tlog)
+                            *reinterpret_cast<uint4*>(&pc.tlog[4 * (size_t)pix]) =
+                                make_uint4(pt0, (uint32_t)__builtin_amdgcn_s_memrealtime(), psteps, pnsh);
                         out[pix] = (COUNT && pc.cost_map)
-                                       ? cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris - work0
+                                       ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
+                                                           : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
+                                             work0
                                        : pack_pixel(col, a.out_recip);
                         has_pix = false;
                     }
@@ -816,7 +896,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds
             // (latency of the few remaining pixels over lane efficiency)
             const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
-            if (COUNT) {
+            if (COUNT || PROF >= 3) {
                 if (!vote || !leaf_round) { ++rs_nr; rs_nl += (uint64_t)__popcll(at_node); }
                 if (!vote || leaf_round) { ++rs_lr; rs_ll += (uint64_t)__popcll(at_leaf); }
             }
@@ -830,7 +910,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
                     in_query = false;
                 }
-                if (pc.cost_out) ++psteps;
+                if (pc.cost_out || (PROF && pc.tlog)) ++psteps;
             }
             if (PROF) {
                 const uint64_t t = stamp();
@@ -852,6 +932,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             atomicAdd(&counters[2], (unsigned long long)nt);
             atomicAdd(&counters[4], (unsigned long long)nvs);
             atomicAdd(&counters[5], (unsigned long long)nts);
+        }
+        if (COUNT || PROF >= 3) {
             atomicAdd(&counters[6], (unsigned long long)rs_nr);
             atomicAdd(&counters[7], (unsigned long long)rs_nl);
             atomicAdd(&counters[8], (unsigned long long)rs_lr);
@@ -872,6 +954,21 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             atomicAdd(&counters[19], (unsigned long long)ps_start);
         }
     }
+}
+
+// TMPT_PAIR=<h>: every 64-rank chunk takes h ranks from the expensive end of the
+// order and 64-h from the cheap end, so a wave's cheap pixels finish early and
+// its lanes then help (HELP) with the expensive ones' shadow queries.
+__global__ void __launch_bounds__(256) k_pair_order(const uint32_t* __restrict__ order, int64_t P, int32_t h,
+                                                     uint32_t* __restrict__ paired)
+{
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= P) return;
+    const int64_t full = P / 64, c = r / 64, i = r - c * 64;
+    const int64_t m = c < full ? 64 : P - full * 64;  // ranks in this chunk
+    const int64_t hc = c < full ? h : (m * h + 63) / 64;  // expensive ranks in this chunk
+    const int64_t src = i < hc ? c * h + i : P - 1 - (c * (64 - h) + (i - hc));
+    paired[r] = order[src];
 }
 
 // Pilot ordering: 3x3 box sum of each pixel's pilot-pass traversal steps,
@@ -1196,11 +1293,15 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3) TMPT_PF(true, 4)
     TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3) TMPT_PF(false, 4)
 #undef TMPT_PF
+    const PathFn fn_default = fn;
     // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
     const char* pe = getenv("TMPT_PROF");
     const bool prof = pe && atoi(pe) != 0 && !count && fmt == 4;
-    if (prof) fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2>
-                                 : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1>;
+    // TMPT_PROF=2: + shading-round split; 3: + per-round cycle counts (more registers:
+    // the kernel may drop to 3 waves/SIMD, so compare its times only among PROF=3 runs)
+    if (prof) fn = atoi(pe) >= 3 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 3>
+                   : atoi(pe) == 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2>
+                                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1>;
     // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
     if (const char* tune = getenv("TMPT_TUNE")) {
         int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
@@ -1229,8 +1330,24 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     int pilot = 4, ratio10 = 0;
     if (const char* e = getenv("TMPT_PILOT")) pilot = std::max(0, atoi(e));
     if (const char* e = getenv("TMPT_PILOT_RATIO")) ratio10 = std::max(0, atoi(e));
-    const bool ordered = pilot > 0 && !count && !prof && a.smp_begin == 0 && a.smp_end == a.spp &&
+    const bool ordered = pilot > 0 && !count && a.smp_begin == 0 && a.smp_end == a.spp &&
                          a.spp >= 2 * pilot && 10 * P >= (int64_t)ratio10 * grid * kBlk && P < (1ll << 31);
+    // Shadow offload at low load (k_path HELP): with at most ~2.5 pixels per
+    // resident lane the frame is bound by the most expensive pixels' chains, and
+    // 27-28 % of their traversal work is shadow queries, which feed neither the
+    // RNG stream nor the path (main.cpp:57-67).  Lanes without a pixel then trace
+    // other lanes' shadow queries, and (ordered passes) each 64-rank chunk pairs
+    // `pair` expensive ranks with 64-pair cheap ones, whose lanes free up early.
+    // Bench frame (tools/tune.py, TUNE_SHARDS): 1/4 shard 86.4 -> 77.2 ms (pair
+    // 56), 1/8 shard 45.7 -> 43.9 ms (pair 52); at 1/2 and 1/1 it loses (the
+    // extra shading code), so it is off there.  TMPT_HELP=0|1 and TMPT_PAIR=<h>
+    // override the choice.
+    const int64_t lanes = (int64_t)grid * kBlk;
+    int help = ordered && fn == fn_default && fmt == 4 && 2 * P <= 5 * lanes ? 1 : 0;
+    if (const char* e = getenv("TMPT_HELP")) help = atoi(e) != 0 && !count && fmt == 4 && !prof;
+    int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
+    if (const char* e = getenv("TMPT_PAIR")) pair = atoi(e);
+    if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 1>;
     const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
@@ -1242,12 +1359,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // TMPT_COST_MAP=1 (diagnostic, instrumented renders only): the output
     // receives each pixel's traversal work (node visits + triangle tests)
     const char* cm = getenv("TMPT_COST_MAP");
-    pc.cost_map = count && cm && atoi(cm) != 0;
+    pc.cost_map = count && cm ? atoi(cm) : 0;  // 2: shadow-query work only
     pc.heads = heads;
     pc.P = P;
 
     pc.order = nullptr;
     pc.cost_out = nullptr;
+    pc.tlog = nullptr;
     pc.prio_q = 0;
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
@@ -1263,9 +1381,32 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     }
     pc.chunk = std::min<uint32_t>(kChunk, pc.lane_cap);
     pc.nchunks = (uint32_t)((P + pc.chunk - 1) / pc.chunk);
-    if (!ordered) {
-        fn<<<grid, kBlk, 0, s.stream>>>(view(s), a, pc, d_out, (uint32_t*)s.ws, d_counters);
+    // TMPT_TLOG=<file> (PROF builds): per-pixel {start, end, steps, shading rounds}
+    // of the final launch, s_memrealtime ticks (100 MHz), written as raw u32
+    const char* tl = prof ? getenv("TMPT_TLOG") : nullptr;
+    auto final_launch = [&](const RenderArgs& af) -> int {
+        uint32_t* d_tlog = nullptr;
+        if (tl) {
+            TMPT_HIP(hipMalloc(&d_tlog, (size_t)P * 16));
+            TMPT_HIP(hipMemsetAsync(d_tlog, 0, (size_t)P * 16, s.stream));
+        }
+        pc.tlog = d_tlog;
+        fn<<<grid, kBlk, 0, s.stream>>>(view(s), af, pc, d_out, (uint32_t*)s.ws, d_counters);
         TMPT_HIP(hipGetLastError());
+        if (tl) {
+            std::vector<uint32_t> h((size_t)P * 4);
+            TMPT_HIP(hipStreamSynchronize(s.stream));
+            TMPT_HIP(hipMemcpy(h.data(), d_tlog, (size_t)P * 16, hipMemcpyDeviceToHost));
+            (void)hipFree(d_tlog);
+            if (FILE* f = fopen(tl, "wb")) {
+                fwrite(h.data(), 4, h.size(), f);
+                fclose(f);
+            }
+        }
+        return 0;
+    };
+    if (!ordered) {
+        if (final_launch(a)) return -1;
         s.path_launches = 1;
         return 0;
     }
@@ -1292,14 +1433,18 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     a2.prog = state;
     pc.cost_out = nullptr;
     pc.order = which ? tvals : vals;
+    if (pair > 0 && pair < 64 && pc.chunk == 64u) {
+        uint32_t* paired = which ? vals : tvals;
+        k_pair_order<<<(unsigned)((P + 255) / 256), 256, 0, s.stream>>>(pc.order, P, pair, paired);
+        pc.order = paired;
+    }
     // TMPT_PRIO=<d>: waves holding ranks of the first d-th of the order issue at
     // priority 3, the next d-th at 2, the next at 1 (0 = off)
     if (const char* e = getenv("TMPT_PRIO")) {
         const int d = atoi(e);
         if (d > 0) pc.prio_q = (uint32_t)std::max<int64_t>(1, (P + d - 1) / d);
     }
-    fn<<<grid, kBlk, 0, s.stream>>>(view(s), a2, pc, d_out, (uint32_t*)s.ws, d_counters);
-    TMPT_HIP(hipGetLastError());
+    if (final_launch(a2)) return -1;
     s.path_launches = 2;
     return 0;
 }
@@ -1411,6 +1556,11 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
             fprintf(stderr, "k_path wave time: shading %.1f%%, node rounds %.1f%%, leaf rounds %.1f%% "
                             "(%.3g wave-cycles)\n",
                     100.0 * c[13] / tot, 100.0 * c[14] / tot, 100.0 * c[15] / tot, tot);
+            if (c[6] && c[8] && c[10])
+                fprintf(stderr, "  cycles per round: node %.0f (%.1f lanes), leaf %.0f (%.1f lanes), shading %.0f "
+                                "(%.1f lanes shading, %.1f traversing); rounds node %llu leaf %llu shading %llu\n",
+                        (double)c[14] / c[6], (double)c[7] / c[6], (double)c[15] / c[8], (double)c[9] / c[8],
+                        (double)c[13] / c[10], (double)c[11] / c[10], (double)c[12] / c[10], c[6], c[8], c[10]);
             if (c[16] + c[17] + c[18] + c[19])
                 fprintf(stderr, "  shading split: ballots+pixel fetch %.1f%%, shade/finish %.1f%%, camera %.1f%%, "
                                 "query set-up %.1f%% (of all wave time)\n",
