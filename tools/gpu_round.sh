@@ -7,7 +7,7 @@ tag=${1:-run}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
 tail -2 $out/pytest_gpu.log
 timeout -k 10 300 python bench.py > $out/bench.json 2> $out/bench.err
 cat $out/bench.json
