@@ -22,7 +22,8 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 3  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi */
+#define TMPT_ABI_VERSION 4  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+                              4: tmpt_unit_sincos */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -150,6 +151,13 @@ int tmpt_get_stats(const tmpt_scene* scene, tmpt_stats* out);
 /* PNG writer (stbi_write_png with flip-on-write, main.cpp:341-342):
  * rgba rows bottom-up as rendered. */
 int tmpt_write_png(const char* path, const uint8_t* rgba, int32_t width, int32_t height);
+
+/* RandomUnitVector's (cos a, sin a) (maths.cpp:33-36: a = ((k / 2^24) * 2) * kPI,
+ * then libm cosf/sinf) for the RNG keys [key0, key0 + n): out = n x {cos, sin}
+ * (host memory).  device >= 0: computed by the device code the renderers run;
+ * device < 0: the same restatement on the host.  A check hook -- the
+ * reference has no counterpart; tests compare it with the host libm. */
+int tmpt_unit_sincos(int32_t device, uint32_t key0, uint32_t n, float* out);
 
 const char* tmpt_last_error(void);
 int tmpt_abi_version(void);

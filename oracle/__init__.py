@@ -77,6 +77,7 @@ _render = _sig("orc_render", ctypes.c_uint64, [ctypes.c_void_p, ctypes.POINTER(_
 _trace = _sig("orc_trace", None, [ctypes.c_void_p, _f32p, _f32p, _u32p, _f32p,
                                   ctypes.POINTER(ctypes.c_uint64)])
 _sincos = _sig("orc_unit_angle_sincos", None, [ctypes.c_uint32, _f32p, _f32p])
+_sincos_range = _sig("orc_unit_sincos_range", None, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p])
 
 
 def _fp(a):
@@ -117,6 +118,13 @@ def unit_angle_sincos(key24: int):
     c, s = ctypes.c_float(), ctypes.c_float()
     _sincos(key24, ctypes.byref(c), ctypes.byref(s))
     return c.value, s.value
+
+
+def unit_sincos_range(key0: int, n: int) -> np.ndarray:
+    """(cos a, sin a) of the host libm for keys [key0, key0 + n), n x 2 float32."""
+    out = np.empty((n, 2), dtype=np.float32)
+    _sincos_range(key0, n, out.ctypes.data)
+    return out
 
 
 def _cam_arr(c: _Camera) -> np.ndarray:

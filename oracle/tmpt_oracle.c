@@ -93,6 +93,11 @@ void orc_unit_angle_sincos(uint32_t key24, float* c, float* s)
     *s = sinf(a);
 }
 
+void orc_unit_sincos_range(uint32_t key0, uint32_t n, float* out)
+{
+    for (uint32_t i = 0; i < n; ++i) orc_unit_angle_sincos(key0 + i, &out[2 * (size_t)i], &out[2 * (size_t)i + 1]);
+}
+
 void orc_random_unit_vector(uint32_t* state, float out[3]) /* maths.cpp:30-38 */
 {
     float z = orc_random_float01(state) * 2.0f - 1.0f;

@@ -97,6 +97,8 @@ void orc_trace(const orc_scene* s, const float orig[3], const float dir[3],
 /* (cos a, sin a) for the 24-bit RNG key k, with a = ((k/2^24)*2)*kPI exactly as
  * RandomUnitVector computes it (maths.cpp:33-36). */
 void orc_unit_angle_sincos(uint32_t key24, float* c, float* s);
+/* the same for keys [key0, key0 + n): out = n x {cos, sin} */
+void orc_unit_sincos_range(uint32_t key0, uint32_t n, float* out);
 
 #ifdef __cplusplus
 }

@@ -508,3 +508,13 @@ def test_cli_reproduces_reference_binary(gpu, tmp_path, name):
     want_sha, want_krays = REFERENCE_BINARY[name]
     assert sha == want_sha
     assert f"- {want_krays:.1f} K Rays" in r.stdout
+
+
+def test_unit_sincos_device_matches_host_libm_every_key(gpu):
+    """The device's cosf/sinf restatement (no libm table) equals the host libm
+    on all 2^24 RNG keys of RandomUnitVector (maths.cpp:33-36)."""
+    n = 1 << 24
+    dev = tm.unit_sincos(0, n, device=0)
+    ref = oracle.unit_sincos_range(0, n)
+    bad = np.nonzero((dev.view(np.uint32) != ref.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} keys differ, first {bad[:8]}"

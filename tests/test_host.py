@@ -163,3 +163,14 @@ def test_parallel_png_same_pixels_as_sequential(tmp_path, monkeypatch):
     a = np.asarray(Image.open(tmp_path / "a.png").convert("RGBA"))
     b = np.asarray(Image.open(tmp_path / "b.png").convert("RGBA"))
     assert np.array_equal(a, b) and np.array_equal(a, img[::-1])
+
+
+def test_unit_sincos_restatement_matches_host_libm_every_key():
+    """RandomUnitVector's cosf/sinf (maths.cpp:35-36): the restatement of glibc's
+    algorithm the device runs (tmpt_math.h glibc_sincosf_unit), evaluated on the
+    host, equals the host libm bit for bit on all 2^24 reachable angles."""
+    n = 1 << 24
+    mine = tm.unit_sincos(0, n, device=-1)
+    ref = oracle.unit_sincos_range(0, n)
+    bad = np.nonzero((mine.view(np.uint32) != ref.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} keys differ, first {bad[:8]}"

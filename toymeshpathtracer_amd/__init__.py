@@ -130,12 +130,14 @@ _stats = _sig("tmpt_get_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_
 _write_png = _sig("tmpt_write_png", ctypes.c_int, [ctypes.c_char_p, _u8p, ctypes.c_int32, ctypes.c_int32])
 _last_error = _sig("tmpt_last_error", ctypes.c_char_p, [])
 _abi = _sig("tmpt_abi_version", ctypes.c_int, [])
+_unit_sincos = _sig("tmpt_unit_sincos", ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
+                                                       ctypes.c_void_p])
 
 #: every symbol include/tmpt.h declares (checked by tests/test_abi.py)
 EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_scene",
            "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_destroy", "tmpt_scene_hit",
            "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
-           "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version")
+           "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos")
 
 
 def _check(rc: int, what: str) -> None:
@@ -145,6 +147,14 @@ def _check(rc: int, what: str) -> None:
 
 def _fp(a: np.ndarray):
     return a.ctypes.data_as(_f32p)
+
+
+def unit_sincos(key0: int, n: int, device: int = 0) -> np.ndarray:
+    """RandomUnitVector's (cos a, sin a) for RNG keys [key0, key0 + n) (maths.cpp:33-36),
+    n x 2 float32: computed on `device`, or by the host restatement when device < 0."""
+    out = np.empty((n, 2), dtype=np.float32)
+    _check(_unit_sincos(device, key0, n, out.ctypes.data), "tmpt_unit_sincos")
+    return out
 
 
 def device_count() -> int:

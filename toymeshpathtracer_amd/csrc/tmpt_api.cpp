@@ -29,6 +29,16 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
                     float* d_hits, int32_t* d_ids);
 
+// RandomUnitVector's (cos a, sin a) over a key range, as the renderers compute it
+__global__ void k_unit_sincos(uint32_t key0, uint32_t n, float2* out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float c, s;
+    glibc_sincosf_unit(unit_angle((key0 + i) & 0xFFFFFFu), c, s);
+    out[i] = make_float2(c, s);
+}
+
 }  // namespace tmpt
 
 struct tmpt_scene {
@@ -62,6 +72,34 @@ extern "C" {
 int tmpt_abi_version(void) { return TMPT_ABI_VERSION; }
 const char* tmpt_last_error(void) { return last_error(); }
 void tmpt_free(void* p) { free(p); }
+
+int tmpt_unit_sincos(int32_t device, uint32_t key0, uint32_t n, float* out)
+{
+    TMPT_GUARD_BEGIN
+    if (!out && n) return bad("tmpt_unit_sincos: null argument");
+    if (n == 0) return 0;
+    if (device < 0) {
+        for (uint32_t i = 0; i < n; ++i)
+            glibc_sincosf_unit(unit_angle((key0 + i) & 0xFFFFFFu), out[2 * (size_t)i], out[2 * (size_t)i + 1]);
+        return 0;
+    }
+    int ndev = 0;
+    TMPT_HIP(hipGetDeviceCount(&ndev));
+    if (device >= ndev) return bad("tmpt_unit_sincos: no such device");
+    TMPT_HIP(hipSetDevice(device));
+    float2* d = nullptr;
+    TMPT_HIP(hipMalloc(&d, sizeof(float2) * (size_t)n));
+    k_unit_sincos<<<(n + 255u) / 256u, 256>>>(key0, n, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, d, sizeof(float2) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) {
+        set_error(std::string("tmpt_unit_sincos: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+    TMPT_GUARD_END
+}
 
 int tmpt_load_obj(const char* path, float** out_tris, int32_t* out_n, float out_bmin[3],
                   float out_bmax[3])
@@ -128,8 +166,6 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
     };
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess)
         return fail((set_error("hipStreamCreate failed"), -1));
-    s.sincos = device_sincos_table(device);
-    if (!s.sincos) return fail(-1);
     float* d_tris = nullptr;
     if (n > 0) {
         if (hipMalloc(&d_tris, sizeof(float) * 9 * (size_t)n) != hipSuccess)

@@ -971,44 +971,4 @@ int build_lbvh(Scene& s, const float* d_tris9)
     return 0;
 }
 
-// ---------------------------------------------------------------- sin/cos table
-// (cos a, sin a) for all 2^24 RNG keys of RandomUnitVector (maths.cpp:33-36),
-// computed by the host's libm so the device reproduces it exactly.
-const float2* device_sincos_table(int device)
-{
-    static std::mutex mu;
-    static std::vector<float2*> tables;
-    static std::vector<float2> host;
-    std::lock_guard<std::mutex> lock(mu);
-    if ((int)tables.size() <= device) tables.resize(device + 1, nullptr);
-    if (tables[device]) return tables[device];
-    const size_t N = size_t(1) << 24;
-    if (host.empty()) {
-        host.resize(N);
-        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < nt; ++t)
-            th.emplace_back([t, nt]() {
-                size_t b = N * t / nt, e = N * (t + 1) / nt;
-                for (size_t k = b; k < e; ++k) {
-                    float a = unit_angle((uint32_t)k);
-                    host[k] = make_float2(cosf(a), sinf(a));
-                }
-            });
-        for (auto& x : th) x.join();
-    }
-    float2* d = nullptr;
-    if (hipMalloc(&d, N * sizeof(float2)) != hipSuccess) {
-        set_error("sincos table: hipMalloc failed");
-        return nullptr;
-    }
-    if (hipMemcpy(d, host.data(), N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        set_error("sincos table: upload failed");
-        return nullptr;
-    }
-    tables[device] = d;
-    return d;
-}
-
 }  // namespace tmpt

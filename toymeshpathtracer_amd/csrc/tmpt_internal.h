@@ -8,8 +8,6 @@
 //                                        original index (the Moller-Trumbore operands)
 //   tri_orig TriOrig[n]           48 B  original order: v0, v1, v2 and the geometric
 //                                        normal, read once per accepted hit
-//   sincos   float2[2^24]        128 MB (cos a, sin a) of RandomUnitVector's angle,
-//                                        filled from the host libm (shared per device)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -115,7 +113,6 @@ struct Scene {
     TriPre* tri_pre = nullptr;
     ShadowGrid sgrid;  // shadow-query grid (tmpt_shadow.hip), R = 0 if none
     TriOrig* tri_orig = nullptr;
-    const float2* sincos = nullptr;  // borrowed from the per-device table
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
     // render workspace (grown on demand, reused across calls)
@@ -160,8 +157,6 @@ size_t radix_sort_hist_words(int32_t n);
 // shadow-query grid (tmpt_shadow.hip); host_tris = the n x 9 input floats
 int build_shadow_grid(Scene& s, const float* host_tris);
 void free_shadow_grid(Scene& s);
-// sincos table for the current device (created on first use, never freed)
-const float2* device_sincos_table(int device);
 
 TMPT_HD float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 

@@ -79,17 +79,72 @@ TMPT_HD f3 random_in_unit_disk(uint32_t& state)
 // Angle of RandomUnitVector for a 24-bit key, maths.cpp:34: (r * 2) * kPI.
 TMPT_HD float unit_angle(uint32_t key24) { return key_to_float01(key24) * 2.0f * kPI; }
 
-// RandomUnitVector, maths.cpp:30-38, with (cos a, sin a) taken from the
-// host-libm table indexed by the 24-bit RNG key of the second draw: the
-// table makes the device reproduce the host's libm bit for bit
-// (SURVEY.md §0.5).
-TMPT_HD f3 random_unit_vector(uint32_t& state, const float2* sincos_lut)
+// cosf / sinf of the host libm (glibc 2.35: sysdeps/ieee754/flt-32/s_sinf.c,
+// s_cosf.c, sincosf.h, sincosf_data.c -- the ARM optimized-routines
+// algorithm) restated for the angles RandomUnitVector produces (0 <= a < 2pi,
+// so only the |a| < 2^-12, |a| < pi/4 and |a| < 120 paths): the float is
+// widened to double, reduced by n = round(a * 2/pi) with the 2^24-scaled
+// integer trick of the non-TOINT_INTRINSICS build, and the sine or cosine
+// polynomial is evaluated in double, then rounded to float once.  The
+// result is bit-identical to the host's cosf/sinf for all 2^24 keys (the
+// glibc FMA and SSE2 variants alike; tests/test_host.py checks every key on
+// the host, tests/test_gpu_parity.py on the device), so the device needs no
+// libm table.
+TMPT_HD float glibc_sincosf_poly(double x, double x2, bool neg, int n)
+{
+    if ((n & 1) == 0) {  // sine polynomial
+        const double x3 = x * x2;
+        const double s1 = __builtin_fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+        const double x7 = x3 * x2;
+        const double s = __builtin_fma(x3, -0x1.555545995a603p-3, x);
+        return (float)__builtin_fma(x7, s1, s);
+    }
+    // cosine polynomial (negated in the table entry of quadrants 2 and 3)
+    const double g = neg ? -1.0 : 1.0;
+    const double x4 = x2 * x2;
+    const double c2 = __builtin_fma(x2, g * 0x1.99343027bf8c3p-16, g * -0x1.6c087e89a359dp-10);
+    const double c1 = __builtin_fma(x2, g * -0x1.ffffffd0c621cp-2, g);
+    const double x6 = x4 * x2;
+    const double c = __builtin_fma(x4, g * 0x1.55553e1068f19p-5, c1);
+    return (float)__builtin_fma(x6, c2, c);
+}
+
+TMPT_HD uint32_t glibc_abstop12(float f) { return (__builtin_bit_cast(uint32_t, f) >> 20) & 0x7FFu; }
+
+TMPT_HD void glibc_sincosf_unit(float a, float& c, float& s)
+{
+    const double x = a;
+    if (glibc_abstop12(a) < glibc_abstop12(0x1.921FB6p-1f)) {  // |a| < pi/4
+        if (glibc_abstop12(a) < glibc_abstop12(0x1p-12f)) {
+            s = a;
+            c = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        s = glibc_sincosf_poly(x, x2, false, 0);
+        c = glibc_sincosf_poly(x, x2, false, 1);
+        return;
+    }
+    // reduce_fast: r = a * (2/pi * 2^24), n = (int(r) + 2^23) >> 24
+    const double r = x * 0x1.45F306DC9C883p+23;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    const double xr = __builtin_fma(-(double)n, 0x1.921FB54442D18p0, x);
+    const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -xr : xr;  // sign[n & 3] = {1, -1, -1, 1}
+    const double x2 = xr * xr;
+    const bool neg = (n & 2) != 0;
+    s = glibc_sincosf_poly(xs, x2, neg, n);
+    c = glibc_sincosf_poly(xs, x2, neg, n ^ 1);
+}
+
+// RandomUnitVector, maths.cpp:30-38 (cosf/sinf of the host libm, above).
+TMPT_HD f3 random_unit_vector(uint32_t& state)
 {
     float z = random_float01(state) * 2.0f - 1.0f;
     uint32_t key = xorshift32(state) & 0xFFFFFFu;
     float r = sqrtf(1.0f - z * z);
-    float2 cs = sincos_lut[key];
-    return mk(r * cs.x, r * cs.y, z);
+    float cs, sn;
+    glibc_sincosf_unit(unit_angle(key), cs, sn);
+    return mk(r * cs, r * sn, z);
 }
 
 // Per-pixel seed (DESIGN.md "RNG seeding"): main.cpp:204's y*9781+1 applied

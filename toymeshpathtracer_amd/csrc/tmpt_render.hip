@@ -125,7 +125,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
                 if (sid >= 0) lc = 0.0f;
             }
             lbuf[depth * BLOCK] = lc;
-            f3 rnd = random_unit_vector(rng, sv.sincos);  // main.cpp:71-72
+            f3 rnd = random_unit_vector(rng);  // main.cpp:71-72
             f3 target = pos + nrm + rnd;
             d = normalize(target - pos);
             o = pos;
@@ -463,7 +463,7 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
                 hit_record(sv, id, s.hit[P + p], s.hit[2 * P + p], pos, nrm);
                 s.light[(int64_t)depth * P + p] = light_cosine(nrm, d);  // zeroed by shadow if occluded
                 s.sho[p] = pos.x; s.sho[P + p] = pos.y; s.sho[2 * P + p] = pos.z;
-                f3 rnd = random_unit_vector(rng, sv.sincos);
+                f3 rnd = random_unit_vector(rng);
                 f3 target = pos + nrm + rnd;
                 d = normalize(target - pos);
                 s.ray[p] = pos.x; s.ray[P + p] = pos.y; s.ray[2 * P + p] = pos.z;
@@ -732,7 +732,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         hit_record(sv, ts.best, ts.bu, ts.bv, pos, nrm);
                         const float lc = light_cosine(nrm, r.d);
                         light[depth * BLOCK] = lc;  // zeroed if occluded
-                        f3 rnd = random_unit_vector(rng, sv.sincos);
+                        f3 rnd = random_unit_vector(rng);
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
@@ -1025,7 +1025,7 @@ int ensure_ws(Scene& s, size_t bytes)
 SceneView view(const Scene& s)
 {
     SceneView v{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
-                s.tri_orig, s.sincos, s.n, s.sgrid, s.n_nodes4};
+                s.tri_orig, s.n, s.sgrid, s.n_nodes4};
     const char* e = getenv("TMPT_SHADOW_GRID");  // 0: keep the grid out of the queries (A/B)
     if (e && atoi(e) == 0) v.sg.R = 0;
     return v;

@@ -136,7 +136,6 @@ struct SceneView {
     const char* __restrict__ nodes4f;  // Bvh4FNode array, addressed by byte offset
     const TriPre* __restrict__ tri_pre;
     const TriOrig* __restrict__ tri_orig;
-    const float2* __restrict__ sincos;
     int32_t n;
     ShadowGrid sg;  // by value: axes, origin, scale, device arrays (R = 0: none)
     int32_t n_nodes4 = 0;
