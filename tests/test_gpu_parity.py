@@ -382,7 +382,9 @@ def test_bench_frame_full_size_shards(gpu, sponza_path):
 
 @pytest.mark.parametrize("env", [{}, {"TMPT_HELP": "0"}, {"TMPT_HELP": "1", "TMPT_PAIR": "0"},
                                  {"TMPT_HELP": "1", "TMPT_PAIR": "40", "TMPT_WAVE_CAP": "48"},
-                                 {"TMPT_HELP": "1", "TMPT_PILOT": "0"}])
+                                 {"TMPT_HELP": "1", "TMPT_PILOT": "0"},
+                                 {"TMPT_BALANCE": "0"}, {"TMPT_DPRIO": "0,0,0"},
+                                 {"TMPT_HELP": "0", "TMPT_DPRIO": "400,200,100"}])
 def test_shadow_offload_matches_oracle(gpu, monkeypatch, env):
     """Low-load shadow offload (k_path HELP: idle lanes trace other lanes' shadow
     queries; pending light slots; paired expensive/cheap chunks).  A small frame
@@ -403,17 +405,21 @@ def test_shadow_offload_matches_oracle(gpu, monkeypatch, env):
 
 
 def test_shadow_offload_bench_frame_shard(gpu, monkeypatch, sponza_path):
-    """The bench frame's 1/8 and 1/4 shards (where the offload is on by default)
-    equal the same shards rendered with it forced off, bit for bit."""
+    """The bench frame's 1/8 and 1/4 shards (where the offload, the SIMD-balanced
+    first chunks and the dynamic priority are on by default) equal the same
+    shards rendered with all three forced off, bit for bit."""
     tris, bmin, bmax = tm.load_scene(sponza_path)
     w, h, spp = 1920, 1080, 64
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
     with tm.Scene(tris) as sc:
         for n in (8, 4):
-            monkeypatch.delenv("TMPT_HELP", raising=False)
+            for k in ("TMPT_HELP", "TMPT_BALANCE", "TMPT_DPRIO"):
+                monkeypatch.delenv(k, raising=False)
             a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=n - 1,
                                    num_shards=n)
             monkeypatch.setenv("TMPT_HELP", "0")
+            monkeypatch.setenv("TMPT_BALANCE", "0")
+            monkeypatch.setenv("TMPT_DPRIO", "0,0,0")
             b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=n - 1,
                                    num_shards=n)
             assert ra == rb and np.array_equal(a, b)

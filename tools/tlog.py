@@ -19,17 +19,21 @@ shards = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 for kv in sys.argv[2:]:
     k, _, v = kv.partition("=")
     os.environ[k] = v
+PROD = os.environ.pop("TMPT_PROF", "1") == "0"  # TMPT_PROF=0: the production kernel
 W, H, SPP = 1920, 1080, 64
 tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
 cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
 sc = tm.Scene(tris)
 path = os.path.join(tempfile.gettempdir(), f"tlog_{os.getpid()}.bin")
-os.environ["TMPT_PROF"] = "1"
+if not PROD:
+    os.environ["TMPT_PROF"] = "1"
 os.environ["TMPT_TLOG"] = path
 img, rays = sc.trace_image(cam, W, H, SPP, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=0, num_shards=shards)
 st = sc.stats()
 t = np.fromfile(path, dtype=np.uint32).reshape(-1, 4).astype(np.int64)
 os.unlink(path)
+if os.environ.get("TLOG_SAVE"):
+    np.save(os.environ["TLOG_SAVE"], t.astype(np.uint32))
 t0 = t[:, 0].min()
 s, e, steps, nsh = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, t[:, 2], t[:, 3]  # us
 dur = e - s

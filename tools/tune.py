@@ -21,7 +21,7 @@ import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
 BUILD_KEYS = ("TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
-RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR")
+RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
@@ -85,4 +85,6 @@ for r in range(rounds):
 for v, xs in res.items():
     a = np.array(xs)
     print(f"{v or 'default':>48}: {np.median(a[:, 0]):8.1f} MRays/s  extend {np.median(a[:, 1]):7.1f} ms  "
-          f"shadow {np.median(a[:, 2]):7.1f} ms  frame {np.median(a[:, 3]):7.1f} ms", flush=True)
+          f"shadow {np.median(a[:, 2]):7.1f} ms  frame {np.median(a[:, 3]):7.1f} ms"
+          + (f"  (render ms mean {a[:, 1].mean():.2f} sd {a[:, 1].std():.2f} min {a[:, 1].min():.2f}, n={len(a)}: "
+             + " ".join(f"{x:.1f}" for x in a[:, 1]) + ")" if len(a) > 2 else ""), flush=True)

@@ -551,15 +551,64 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 struct PathCtl {
     uint32_t* heads;  // kSeg chunk counters, stride kCtr
     uint32_t nchunks;
+    // SIMD-balanced first chunks (ordered pass, cost-descending chunks): the
+    // wave of rank r on the d-th SIMD to register takes chunk r*nsimd + d (r
+    // even) or r*nsimd + nsimd-1-d (r odd), so every SIMD's resident waves sum
+    // to about the same work.  Every chunk has a claim word: the first chunk
+    // and the segment supply both claim, so a chunk the placement left
+    // unassigned (uneven waves per SIMD) is still taken, and none twice.
+    // simd_reg = 2 words per hardware SIMD key (waves seen, dense index + 1)
+    // plus a dense counter at kSimdKeys*2.  null = off.
+    uint32_t* simd_reg;
+    uint32_t* claim;  // nchunks words, zeroed per launch
+    uint32_t nsimd, wps;
     int64_t P;
     int cost_map;                     // COUNT only: write per-pixel traversal work instead of colour
     const uint32_t* __restrict__ order;  // rank -> pixel, or null
     uint32_t* __restrict__ cost_out;     // per-pixel traversal steps of this call, or null
     uint32_t prio_q;  // ordered pass: ranks per wave-priority level (s_setprio 3..0), 0 = off
+    // dynamic issue priority (longest remaining first): each shading round the
+    // wave estimates its lanes' remaining traversal steps (steps so far per
+    // finished sample x samples left) and sets s_setprio 3/2/1/0 at the
+    // thresholds dprio[0] > dprio[1] > dprio[2] (steps); dprio[0] = 0: off.
+    // With dprio_cost (the pilot pass's per-pixel steps), the thresholds are
+    // fractions of the heaviest pixel's (order[0]) projected remaining steps.
+    float dprio[3];
+    const uint32_t* __restrict__ dprio_cost;
     uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
     uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
     uint32_t* __restrict__ tlog;  // PROF: per pixel {start, end (s_memrealtime), steps, shading rounds}
 };
+
+constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
+
+// Rank of this wave among the waves resident on its SIMD -- its hardware wave
+// slot, which the dispatcher fills oldest first, so rank 0 is the wave the
+// SIMD's arbiter favours (oldest first) -- and the SIMD's dense registration
+// index (PathCtl::simd_reg).  Lane 0 registers; the first wave of a SIMD to
+// arrive draws the dense index and publishes it, later ones wait for it (it
+// is already running: it won the claim before them).
+__device__ __forceinline__ uint2 simd_rank(uint32_t* reg)
+{
+    uint32_t r = 0, d = 0;
+    if (lane_id() == 0) {
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // XCC_ID
+        const uint32_t key = ((((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u +
+                               ((hw >> 8) & 15u)) * 4u) + ((hw >> 4) & 3u);
+        r = hw & 15u;  // wave slot
+        if (atomicAdd(&reg[2 * key], 1u) == 0) {
+            d = atomicAdd(&reg[2 * kSimdKeys], 1u);
+            __hip_atomic_store(&reg[2 * key + 1], d + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            uint32_t v;
+            while ((v = __hip_atomic_load(&reg[2 * key + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                __builtin_amdgcn_s_sleep(2);
+            d = v - 1u;
+        }
+    }
+    return make_uint2((uint32_t)__shfl((int)r, 0), (uint32_t)__shfl((int)d, 0));
+}
 
 constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per block (7.5 KB)
 
@@ -590,6 +639,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         st.top = (const lds_u4*)s_top;
         st.ntop = ntop;
     }
+    float dp0 = pc.dprio[0], dp1 = pc.dprio[1], dp2 = pc.dprio[2];
+    if (pc.dprio_cost && pc.order && a.smp_begin > 0) {  // relative thresholds (wave-uniform)
+        const float sc = (float)pc.dprio_cost[pc.order[0]] * (float)(a.smp_end - a.smp_begin) / (float)a.smp_begin;
+        dp0 *= sc;
+        dp1 *= sc;
+        dp2 *= sc;
+    }
     TravCount cnt, cnt_s;  // COUNT: closest-hit and shadow queries apart
     uint32_t rays_e = 0, rays_s = 0;
     const f3 ldir = light_dir();
@@ -597,6 +653,26 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
     uint32_t res = 0, res_end = 0;
     bool exhausted = pc.P == 0;
+    if (pc.simd_reg && !exhausted) {  // SIMD-balanced first chunk
+        const uint2 rd = simd_rank(pc.simd_reg);
+        if (rd.x < pc.wps && rd.y < pc.nsimd) {
+            const uint32_t c = rd.x * pc.nsimd + ((rd.x & 1u) ? pc.nsimd - 1u - rd.y : rd.y);
+            uint32_t got = 0;
+            if (c < pc.nchunks && lane_id() == 0) got = atomicExch(&pc.claim[c], 1u) == 0u;
+            if (__shfl((int)got, 0)) {
+                res = c * pc.chunk;
+                res_end = (uint32_t)min<int64_t>((int64_t)res + pc.chunk, pc.P);
+            } else if (c < pc.nchunks && lane_id() == 0) {
+                atomicAdd(&counters[21], 1ull);  // balance diagnostics: lost the claim
+            }
+        } else if (lane_id() == 0) {
+            atomicAdd(&counters[20 + (rd.x >= pc.wps ? 2 : 3)], 1ull);  // slot beyond wps / no dense index
+        }
+        // a wave left without a first chunk waits ~20 us before the segment
+        // supply, so it does not take a chunk another wave is about to claim
+        if (res >= res_end)
+            for (int k = 0; k < 6; ++k) __builtin_amdgcn_s_sleep(127);
+    }
     bool has_pix = false, in_query = false, qany = false;
     // HELP (shadow offload to idle lanes): once the pixel supply is exhausted, a
     // lane without a pixel becomes a helper that traces another lane's shadow
@@ -662,6 +738,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         if (lane_id() == 0) b = atomicAdd(&pc.heads[seg * kCtr], 1u);
                         b = (uint32_t)__shfl((int)b, 0);
                     }
+                    if (b < c && pc.claim) {  // taken as some wave's balanced first chunk?
+                        uint32_t got = 0;
+                        if (lane_id() == 0) got = atomicExch(&pc.claim[seg + b * (uint32_t)kSeg], 1u) == 0u;
+                        if (!__shfl((int)got, 0)) continue;
+                    }
                     if (b < c) {
                         res = (seg + b * (uint32_t)kSeg) * pc.chunk;
                         res_end = (uint32_t)min<int64_t>((int64_t)res + pc.chunk, pc.P);
@@ -688,6 +769,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         pt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         pnsh = 0;
                     }
+                    if (!PROF && pc.tlog) pc.tlog[4 * (size_t)pix] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
@@ -836,6 +918,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         if (PROF && pc.tlog)
                             *reinterpret_cast<uint4*>(&pc.tlog[4 * (size_t)pix]) =
                                 make_uint4(pt0, (uint32_t)__builtin_amdgcn_s_memrealtime(), psteps, pnsh);
+                        if (!PROF && pc.tlog) {  // start was stored at the fetch
+                            pc.tlog[4 * (size_t)pix + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                            pc.tlog[4 * (size_t)pix + 2] = psteps;
+                            // where it ran: XCC_ID << 16 | HW_ID[15:0] (wave, SIMD, CU, SH, SE)
+                            pc.tlog[4 * (size_t)pix + 3] = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) |
+                                                           (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu);
+                        }
                         out[pix] = (COUNT && pc.cost_map)
                                        ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
                                                            : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
@@ -879,6 +968,19 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
         }
+        if (dp0 > 0.0f) {  // longest remaining traversal work first (wave-uniform)
+            float rem = 0.0f;
+            if (has_pix)
+                rem = smp > (uint32_t)a.smp_begin
+                          ? (float)psteps * (float)((uint32_t)a.smp_end - smp) *
+                                __builtin_amdgcn_rcpf((float)(smp - (uint32_t)a.smp_begin))
+                          : 3.0e38f;
+            for (int o = 32; o > 0; o >>= 1) rem = fmaxf(rem, __shfl_xor(rem, o));
+            if (rem >= dp0) __builtin_amdgcn_s_setprio(3);
+            else if (rem >= dp1) __builtin_amdgcn_s_setprio(2);
+            else if (rem >= dp2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (PROF) {
             const uint64_t t = stamp();
             pt_shade += t - pt_t;
@@ -910,7 +1012,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
                     in_query = false;
                 }
-                if (pc.cost_out || (PROF && pc.tlog)) ++psteps;
+                if (pc.cost_out || pc.tlog || dp0 > 0.0f) ++psteps;
             }
             if (PROF) {
                 const uint64_t t = stamp();
@@ -1317,6 +1419,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
     }
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    // TMPT_BLOCKS_PER_CU=<b> (A/B): fewer resident blocks than the occupancy allows
+    if (const char* e = getenv("TMPT_BLOCKS_PER_CU")) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) == hipSuccess && cus > 0 &&
+            atoi(e) > 0)
+            grid = std::min(grid, atoi(e) * cus);
+    }
     const int64_t P = a.slots;
     // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
     // a shard has several pixels per resident lane, the frame ends with the
@@ -1351,7 +1460,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
-    const size_t extra_words = ordered ? (size_t)P * (4 + 5) + hist_words : 0;
+    const size_t reg_words = ordered ? 2 * (size_t)kSimdKeys + 64 + (size_t)P : 0;  // + claim words
+    const size_t extra_words = ordered ? (size_t)P * (4 + 5) + hist_words + reg_words : 0;
     if (ensure_ws(s, (ovf_words + head_words + extra_words) * 4)) return -1;
     uint32_t* heads = (uint32_t*)s.ws + ovf_words;
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
@@ -1362,11 +1472,16 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.cost_map = count && cm ? atoi(cm) : 0;  // 2: shadow-query work only
     pc.heads = heads;
     pc.P = P;
+    pc.simd_reg = nullptr;
+    pc.claim = nullptr;
+    pc.nsimd = pc.wps = 0;
 
     pc.order = nullptr;
     pc.cost_out = nullptr;
     pc.tlog = nullptr;
     pc.prio_q = 0;
+    pc.dprio[0] = pc.dprio[1] = pc.dprio[2] = 0.0f;
+    pc.dprio_cost = nullptr;
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
     // slots and each wave's chain -- the frame's critical path at that load --
@@ -1381,9 +1496,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     }
     pc.chunk = std::min<uint32_t>(kChunk, pc.lane_cap);
     pc.nchunks = (uint32_t)((P + pc.chunk - 1) / pc.chunk);
-    // TMPT_TLOG=<file> (PROF builds): per-pixel {start, end, steps, shading rounds}
+    // TMPT_TLOG=<file>: per-pixel {start, end, steps, shading rounds} (the
+    // shading-round count in PROF builds only)
     // of the final launch, s_memrealtime ticks (100 MHz), written as raw u32
-    const char* tl = prof ? getenv("TMPT_TLOG") : nullptr;
+    const char* tl = getenv("TMPT_TLOG");
     auto final_launch = [&](const RenderArgs& af) -> int {
         uint32_t* d_tlog = nullptr;
         if (tl) {
@@ -1418,6 +1534,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     uint32_t* tkeys = vals + P;
     uint32_t* tvals = tkeys + P;
     uint32_t* hist = tvals + P;
+    uint32_t* simd_reg = hist + hist_words;
     RenderArgs a1 = a;  // pass 1: samples [0, pilot), per-pixel steps
     a1.smp_end = pilot;
     a1.out_recip = 1.0f / (float)pilot;
@@ -1438,11 +1555,52 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         k_pair_order<<<(unsigned)((P + 255) / 256), 256, 0, s.stream>>>(pc.order, P, pair, paired);
         pc.order = paired;
     }
+    // SIMD-balanced first chunks (PathCtl::simd_reg): with the chunks in
+    // descending cost, the resident waves of every SIMD take one chunk from
+    // each quarter, alternating ends, instead of the launch order's heaviest or
+    // lightest of every quarter.  TMPT_BALANCE=0|1.
+    int balance = 1;
+    if (const char* e = getenv("TMPT_BALANCE")) balance = atoi(e) != 0;
+    if (balance) {
+        int dev_cus = 0;
+        if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
+            dev_cus < 1)
+            dev_cus = 256;
+        const uint32_t per_cu = (uint32_t)std::max(1, grid / dev_cus);  // blocks per CU
+        pc.simd_reg = simd_reg;
+        pc.nsimd = (uint32_t)dev_cus * 4u;
+        pc.wps = per_cu * (uint32_t)(kBlk / 64) / 4u;
+        pc.claim = simd_reg + 2 * (size_t)kSimdKeys + 64;
+        TMPT_HIP(hipMemsetAsync(simd_reg, 0, reg_words * 4, s.stream));
+    }
     // TMPT_PRIO=<d>: waves holding ranks of the first d-th of the order issue at
     // priority 3, the next d-th at 2, the next at 1 (0 = off)
     if (const char* e = getenv("TMPT_PRIO")) {
         const int d = atoi(e);
         if (d > 0) pc.prio_q = (uint32_t)std::max<int64_t>(1, (P + d - 1) / d);
+    }
+    // Dynamic priority (PathCtl::dprio) at low load (with the helpers): the
+    // heaviest waves start at the top level and step down as their projected
+    // remaining work falls below 32 / 21 / 10.5 % of the heaviest pixel's, so
+    // the issue slots go to the waves with the most work left instead of to
+    // the oldest.  Bench frame, 1/8 shard 44.9 -> 42.4 ms, 1/4 78.9 -> 75.3 ms
+    // (with the balanced first chunks); at one pixel pass per lane or more it
+    // costs ~0.4 %, so it is off there.  TMPT_DPRIO=<t3>,<t2>,<t1>: absolute
+    // thresholds in steps (0,0,0 = off).
+    if (help) {
+        pc.dprio[0] = 0.32f;
+        pc.dprio[1] = 0.21f;
+        pc.dprio[2] = 0.105f;
+        pc.dprio_cost = cost;
+    }
+    if (const char* e = getenv("TMPT_DPRIO")) {
+        float t3 = 0, t2 = 0, t1 = 0;
+        if (sscanf(e, "%f,%f,%f", &t3, &t2, &t1) == 3) {
+            pc.dprio[0] = t3;
+            pc.dprio[1] = t2;
+            pc.dprio[2] = t1;
+            pc.dprio_cost = nullptr;
+        }
     }
     if (final_launch(a2)) return -1;
     s.path_launches = 2;
@@ -1566,6 +1724,9 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
                                 "query set-up %.1f%% (of all wave time)\n",
                         100.0 * c[16] / tot, 100.0 * c[17] / tot, 100.0 * c[18] / tot, 100.0 * c[19] / tot);
         }
+        if (getenv("TMPT_BALANCE_LOG"))
+            fprintf(stderr, "balance: %.2f ms, lost claims %llu, slots beyond wps %llu, no dense index %llu\n", ms,
+                    c[21], c[22], c[23]);
         if (count && getenv("TMPT_ROUND_LOG"))  // diagnostic: wave-round efficiency
             fprintf(stderr,
                     "k_path rounds: node %llu (%.1f lanes), leaf %llu (%.1f lanes), shade %llu "
