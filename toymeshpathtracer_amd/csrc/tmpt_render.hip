@@ -575,6 +575,7 @@ struct PathCtl {
     // fractions of the heaviest pixel's (order[0]) projected remaining steps.
     float dprio[3];
     const uint32_t* __restrict__ dprio_cost;
+    int diag_noshadow;  // diagnostic (TMPT_DIAG_NOSHADOW=1, wrong images): shadow queries answered "clear" untraced
     uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
     uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
     uint32_t* __restrict__ tlog;  // PROF: per pixel {start, end (s_memrealtime), steps, shading rounds}
@@ -819,7 +820,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 nd = normalize(target - pos);
                         ++depth;
                         bool traced = false;
-                        if (lc > 0.0f) {
+                        if (lc > 0.0f && !pc.diag_noshadow) {
                             // shadow query: with the light-space grid, the triangles of
                             // the origin's cell (one leaf range, tested by the leaf
                             // steps of the traversal rounds); without, the BVH
@@ -1485,6 +1486,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.prio_q = 0;
     pc.dprio[0] = pc.dprio[1] = pc.dprio[2] = 0.0f;
     pc.dprio_cost = nullptr;
+    pc.diag_noshadow = getenv("TMPT_DIAG_NOSHADOW") ? atoi(getenv("TMPT_DIAG_NOSHADOW")) : 0;
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
     // slots and each wave's chain -- the frame's critical path at that load --
