@@ -52,6 +52,7 @@ def _sig(name, res, args):
 
 
 _xorshift = _sig("orc_xorshift32", ctypes.c_uint32, [_u32p])
+_xorshift_jump = _sig("orc_xorshift32_jump", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64])
 _rand01 = _sig("orc_random_float01", ctypes.c_float, [_u32p])
 _disk = _sig("orc_random_in_unit_disk", None, [_u32p, _f32p])
 _unitv = _sig("orc_random_unit_vector", None, [_u32p, _f32p])
@@ -87,6 +88,11 @@ def _fp(a):
 def xorshift_seq(seed: int, n: int) -> np.ndarray:
     s = ctypes.c_uint32(seed)
     return np.array([_xorshift(ctypes.byref(s)) for _ in range(n)], np.uint32)
+
+
+def xorshift_jump(seed: int, n: int) -> int:
+    """State after n xorshift steps from `seed` (GF(2) matrix power, maths.cpp:5-13)."""
+    return int(_xorshift_jump(seed, n))
 
 
 def float01_seq(seed: int, n: int) -> np.ndarray:

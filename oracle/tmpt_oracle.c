@@ -66,6 +66,43 @@ uint32_t orc_xorshift32(uint32_t* state) /* maths.cpp:5-13 */
     return x;
 }
 
+/* Jump-ahead of the maths.cpp:5-13 xorshift by n steps (state after n calls).
+ * One step is linear over GF(2)^32: x' = M x with M = (I+L15)(I+R17)(I+L13).
+ * M^n by square-and-multiply on 32-column bit matrices (column j = image of
+ * bit j).  Checker for the planned per-sample substream seeding mode
+ * (DESIGN.md §6): sample s would start at M^(2^16 s) of the pixel seed. */
+static uint32_t orc_gf2_apply(const uint32_t* m, uint32_t x)
+{
+    uint32_t r = 0;
+    for (int j = 0; j < 32; ++j)
+        if (x >> j & 1u) r ^= m[j];
+    return r;
+}
+
+static void orc_gf2_mul(const uint32_t* a, const uint32_t* b, uint32_t* out) /* out = a*b */
+{
+    uint32_t t[32];
+    for (int j = 0; j < 32; ++j) t[j] = orc_gf2_apply(a, b[j]);
+    memcpy(out, t, sizeof t);
+}
+
+uint32_t orc_xorshift32_jump(uint32_t state, uint64_t n)
+{
+    uint32_t m[32], acc[32];
+    for (int j = 0; j < 32; ++j) {
+        uint32_t x = 1u << j;
+        orc_xorshift32(&x);
+        m[j] = x;
+        acc[j] = 1u << j;
+    }
+    while (n) {
+        if (n & 1u) orc_gf2_mul(m, acc, acc);
+        orc_gf2_mul(m, m, m);
+        n >>= 1;
+    }
+    return orc_gf2_apply(acc, state);
+}
+
 float orc_random_float01(uint32_t* state) /* maths.cpp:15-18 */
 {
     return (float)(orc_xorshift32(state) & 0xFFFFFFu) / 16777216.0f;

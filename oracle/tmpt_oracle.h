@@ -46,6 +46,7 @@ enum { ORC_SEED_ROW = 0, ORC_SEED_PIXEL = 1 };
 
 /* ---- RNG / sampling KATs (maths.cpp:5-38) ---- */
 uint32_t orc_xorshift32(uint32_t* state);
+uint32_t orc_xorshift32_jump(uint32_t state, uint64_t n);
 float    orc_random_float01(uint32_t* state);
 void     orc_random_in_unit_disk(uint32_t* state, float out[3]);
 void     orc_random_unit_vector(uint32_t* state, float out[3]);

@@ -141,6 +141,20 @@ def test_xorshift_independent_restatement():
     assert f == oracle.float01_seq(9781 * 3 + 1, 1000)[-1]
 
 
+@pytest.mark.parametrize("seed", [1, 9781 * 7 + 1, 0xDEADBEEF])
+def test_xorshift_jump_equals_sequential_steps(seed):
+    """GF(2) jump (checker for the planned per-sample substream mode) == n single steps."""
+    seq = oracle.xorshift_seq(seed, 70000)
+    for n in (1, 2, 3, 17, 1000, 65536, 70000):
+        assert oracle.xorshift_jump(seed, n) == int(seq[n - 1])
+    assert oracle.xorshift_jump(seed, 0) == seed
+    # composition: M^(a+b) = M^a M^b, at offsets far past any sequential check
+    a, b = 2**16 * 63, 2**40 + 5
+    assert oracle.xorshift_jump(oracle.xorshift_jump(seed, a), b) == oracle.xorshift_jump(seed, a + b)
+    # period of xorshift32 over nonzero states is 2^32 - 1
+    assert oracle.xorshift_jump(seed, 2**32 - 1) == seed
+
+
 def test_disk_and_unit_vector_properties():
     d, _ = oracle.disk_seq(5, 2000)
     assert (d[:, 2] == 0).all() and ((d[:, :2].astype(np.float64) ** 2).sum(1) < 1).all()
