@@ -137,6 +137,9 @@ def main() -> None:
     image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
 
     def step():
+        # out= a device tile: the render waits for torch's current stream
+        # (TMPT_FLAG_WAIT_STREAM), on which torch orders the previous step's
+        # gather / assembly of the same tile, and returns once the tile is done
         _, rays = scene.trace_image(cam, W, H, SPP, seed_mode=tm.SEED_PIXEL, engine=engine,
                                     band_rows=BAND_ROWS, shard=rank, num_shards=world,
                                     out=tile.data_ptr())

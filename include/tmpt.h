@@ -22,8 +22,9 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 4  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
-                              4: tmpt_unit_sincos */
+#define TMPT_ABI_VERSION 5  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+                              4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
+                              progressive continuation keyed on the camera */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -46,7 +47,8 @@ enum {
 /* render flags */
 enum {
     TMPT_FLAG_OUT_DEVICE = 1,    /* rgba_out is a device pointer on the scene's device */
-    TMPT_FLAG_COUNT_VISITS = 2   /* instrumented traversal: node visits / triangle tests */
+    TMPT_FLAG_COUNT_VISITS = 2,  /* instrumented traversal: node visits / triangle tests */
+    TMPT_FLAG_WAIT_STREAM = 4    /* the render starts after the work enqueued on desc->wait_stream */
 };
 
 /* One render call = one shard of one frame (TraceImageBody over its rows,
@@ -68,9 +70,19 @@ typedef struct {
      * the previous call on this scene left for the same shard, so the passes
      * together equal one full render bit for bit; each pass writes a preview
      * (colour sum / samples so far, main.cpp:221-233 at that count) and the
-     * pass that reaches spp writes the final image. */
+     * pass that reaches spp writes the final image.  The continuation must use
+     * the same camera, size, spp and shard as the pass before it (checked). */
     int32_t spp_begin, spp_count;
-    int32_t reserved[5];
+    int32_t reserved0;
+    /* Stream ordering (TMPT_FLAG_WAIT_STREAM): a hipStream_t of the caller on
+     * the scene's device (0 = its null stream).  The render's kernels run on
+     * the scene's own non-blocking stream; with the flag they start only
+     * after everything enqueued on wait_stream before the call -- e.g. a
+     * collective still reading the device buffer a previous render wrote, or
+     * the caller's fill of it.  The call returns once the render is complete
+     * on the device, so work the caller enqueues afterwards sees the result. */
+    uint64_t wait_stream;
+    int32_t reserved[2];
 } tmpt_render_desc;
 
 /* Statistics of the last render on a scene (HIP-event timed on the scene's

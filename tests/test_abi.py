@@ -42,7 +42,7 @@ def test_no_oracle_or_torch_in_the_product_library():
 
 
 def test_abi_version_and_error_channel():
-    assert tm.abi_version() == 4
+    assert tm.abi_version() == 5
     with pytest.raises(tm.TmptError) as e:
         tm.load_scene("/definitely/missing.obj")
     assert "missing.obj" in str(e.value)
@@ -64,13 +64,13 @@ def test_struct_layouts_match_ctypes(tmp_path):
     src = tmp_path / "s.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tmpt.h"\n'
                    'int main(void){ printf("%zu %zu %zu %zu\\n", sizeof(tmpt_camera), sizeof(tmpt_render_desc),'
-                   ' sizeof(tmpt_stats), offsetof(tmpt_stats, build_ms)); printf("%zu\\n", offsetof(tmpt_render_desc, spp_begin));'
+                   ' sizeof(tmpt_stats), offsetof(tmpt_stats, build_ms)); printf("%zu %zu\\n", offsetof(tmpt_render_desc, spp_begin), offsetof(tmpt_render_desc, wait_stream));'
                    ' return 0; }\n')
     exe = tmp_path / "s"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()
     want = [ctypes.sizeof(tm._Camera), ctypes.sizeof(tm._Desc), ctypes.sizeof(tm._Stats),
-            tm._Stats.build_ms.offset, tm._Desc.spp_begin.offset]
+            tm._Stats.build_ms.offset, tm._Desc.spp_begin.offset, tm._Desc.wait_stream.offset]
     assert list(map(int, got)) == want
 
 

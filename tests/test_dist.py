@@ -1,11 +1,16 @@
-"""The N>1 path on CPU: world_size-2 gloo ranks each render their row bands
-(with the CPU oracle standing in for the device, as a checker only), gather
-the tiles to rank 0 with one collective and assemble the frame with the same
-code bench.py uses -- the result must equal the single-rank frame."""
+"""The N>1 path on CPU: world_size-2 (and 3) gloo ranks each render ONLY their
+shard -- the rows bench.py deals them (1-row bands, round-robin: rows
+rank, rank+N, ...) -- with the CPU oracle standing in for the device (a
+checker only: oracle.Scene.render over that row subset), gather the padded
+tiles to rank 0 with one collective and assemble the frame with the same code
+bench.py uses.  The assembled frame must equal one full-frame render, and the
+shards' ray counts must sum to its count (pixel seeding makes rows
+independent, so a shard render is the full render restricted to its rows)."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from conftest import ROOT, data
@@ -28,28 +33,37 @@ def _worker(rank, world, port, out_path):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    w, h, spp, band = 96, 70, 2, 16
+    w, h, spp, band = 96, 70, 2, 1
     tris, bmin, bmax = oracle.load_scene(data("suzanne.obj"))
     cam = oracle.camera_for_scene(bmin, bmax, w, h)
     sc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX)
     rows = shard.all_rows(h, band, world)
-    full, rays = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_PIXEL)  # rendered rows only below
     mine = rows[rank]
-    frame_part, _ = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_PIXEL, threads=2)
+    assert np.array_equal(mine, np.arange(rank, h, world))  # bench.py's deal at BAND_ROWS = 1
+    # this rank's shard only: rows rank, rank + world, ...
+    part, rays = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_PIXEL, y0=rank, row_step=world, threads=2)
     tile = np.zeros((max(len(r) for r in rows), w, 4), np.uint8)
-    tile[: len(mine)] = frame_part[mine]
+    tile[: len(mine)] = part[mine]
     t = torch.from_numpy(tile)
     gathered = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
     dist.gather(t, gathered, dst=0)
+    r = torch.tensor([rays], dtype=torch.int64)
+    dist.all_reduce(r)
     if rank == 0:
         frame = np.zeros((h, w, 4), np.uint8)
         shard.assemble([g.numpy() for g in gathered], rows, frame)
+        full, full_rays = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_PIXEL, threads=2)
         np.save(out_path, np.stack([frame, full]))
+        np.save(out_path + ".rays.npy", np.array([int(r.item()), full_rays], np.int64))
     dist.destroy_process_group()
 
 
-def test_gloo_two_ranks_assemble_frame(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_render_shards_and_assemble_frame(tmp_path, world):
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     frame, full = np.load(out)
+    assert (full != 0).any()
     assert np.array_equal(frame, full)
+    shard_rays, full_rays = np.load(out + ".rays.npy")
+    assert shard_rays == full_rays

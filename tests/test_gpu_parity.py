@@ -230,6 +230,32 @@ def test_device_output_pointer(gpu):
     sc.close()
 
 
+def test_device_output_ordered_after_caller_stream(gpu):
+    """TMPT_FLAG_WAIT_STREAM (bench.py's N>1 step): two cameras rendered back to
+    back into ONE device tile while torch's stream still has a delayed reader
+    of the first frame queued (a stand-in for the RCCL gather): the reader must
+    see the first frame, and the second render must not start before it."""
+    import torch
+
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    w, h, spp = 160, 90, 2
+    cam_a = tm.Camera.for_scene(bmin, bmax, w, h)
+    cam_b = tm.Camera.create(bmin - (bmax - bmin), (bmin + bmax) / 2, [0, 1, 0], 40.0, w / h, 0.0, 3.0)
+    host_a, _ = sc.trace_image(cam_a, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    host_b, _ = sc.trace_image(cam_b, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    assert not np.array_equal(host_a, host_b)
+    tile = torch.full((h, w, 4), 7, dtype=torch.uint8, device="cuda:0")  # the caller's fill, ordered too
+    seen = []
+    for cam in (cam_a, cam_b):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, out=tile.data_ptr())
+        torch.cuda._sleep(50_000_000)  # the reader waits behind 20-500 ms of GPU time
+        seen.append(tile.clone())
+    torch.cuda.synchronize()
+    assert np.array_equal(seen[0].cpu().numpy(), host_a)
+    assert np.array_equal(seen[1].cpu().numpy(), host_b)
+    sc.close()
+
+
 def test_count_visits_instrumentation(gpu):
     tris, bmin, bmax, sc = _scene("suzanne.obj")
     cam = tm.Camera.for_scene(bmin, bmax, 160, 90)
@@ -293,11 +319,19 @@ def test_progressive_shards_and_errors(gpu):
     w, h, spp = 160, 90, 6
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     full, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=16, shard=1, num_shards=3)
+    full0, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
     *_, (done, img, _) = sc.trace_progressive(cam, w, h, spp, 2, band_rows=16, shard=1, num_shards=3)
     assert done == spp and np.array_equal(img, full)
     # a continuation needs the previous pass of the same shard
     with pytest.raises(tm.TmptError, match="continue"):
         sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=2, spp_count=2)
+    # ... and of the same camera: another camera's samples must not blend in
+    sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=0, spp_count=2)
+    other = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with pytest.raises(tm.TmptError, match="same camera"):
+        sc.trace_image(other, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=2, spp_count=2)
+    img, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, spp_begin=2, spp_count=4)
+    assert np.array_equal(img, full0)
     with pytest.raises(tm.TmptError, match="persistent"):
         sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT,
                        spp_begin=0, spp_count=2)

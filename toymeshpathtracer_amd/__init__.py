@@ -34,7 +34,7 @@ __all__ = [
 
 SEED_ROW, SEED_PIXEL = 0, 1
 ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL, ENGINE_PERSISTENT = 0, 1, 2
-FLAG_OUT_DEVICE, FLAG_COUNT_VISITS = 1, 2
+FLAG_OUT_DEVICE, FLAG_COUNT_VISITS, FLAG_WAIT_STREAM = 1, 2, 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(_HERE, "_lib", "libtmpt.so")
@@ -80,7 +80,8 @@ class _Desc(ctypes.Structure):
                 ("shard", ctypes.c_int32), ("num_shards", ctypes.c_int32),
                 ("engine", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("spp_begin", ctypes.c_int32), ("spp_count", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 5)]
+                ("reserved0", ctypes.c_int32), ("wait_stream", ctypes.c_uint64),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 class _Stats(ctypes.Structure):
@@ -267,13 +268,24 @@ class RenderStats:
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
-          engine=ENGINE_PERSISTENT, flags=0, spp_begin=0, spp_count=0) -> _Desc:
+          engine=ENGINE_PERSISTENT, flags=0, spp_begin=0, spp_count=0, wait_stream=None) -> _Desc:
     d = _Desc()
     d.width, d.height, d.spp, d.seed_mode = width, height, spp, seed_mode
     d.band_rows, d.shard, d.num_shards = band_rows, shard, num_shards
     d.engine, d.flags = engine, flags
     d.spp_begin, d.spp_count = spp_begin, spp_count
+    if wait_stream is not None:
+        d.flags |= FLAG_WAIT_STREAM
+        d.wait_stream = int(wait_stream)
     return d
+
+
+def _current_stream(device: int):
+    """hipStream_t of torch's current stream on `device` (0 = its null stream),
+    or None without torch / a visible GPU."""
+    if torch is None or not torch.cuda.is_available():
+        return None
+    return int(torch.cuda.current_stream(device).cuda_stream)
 
 
 def tile_rows(width, height, band_rows=0, shard=0, num_shards=1) -> int:
@@ -339,15 +351,27 @@ class Scene:
     def trace_image(self, camera: Camera, width: int, height: int, spp: int,
                     seed_mode: int = SEED_ROW, engine: int = ENGINE_PERSISTENT, band_rows: int = 0,
                     shard: int = 0, num_shards: int = 1, count_visits: bool = False,
-                    out=None, spp_begin: int = 0, spp_count: int = 0) -> Tuple[np.ndarray, int]:
+                    out=None, spp_begin: int = 0, spp_count: int = 0,
+                    wait_stream="current") -> Tuple[np.ndarray, int]:
         """Render one shard.  Returns (rgba[tile_rows, width, 4] uint8, rays).
         Row 0 is the lowest rendered row (main.cpp:229; flipped on PNG write).
-        ``out`` may be a device pointer (int) with tile_rows*width*4 bytes.
+        ``out`` may be a device pointer (int) with tile_rows*width*4 bytes; the
+        render then starts after the work already enqueued on ``wait_stream``
+        ("current": torch's current stream on the scene's device, so a fill of
+        ``out`` or a collective still reading it is ordered before the render;
+        an int: a raw hipStream_t; None: no ordering).  The call returns once
+        the frame is complete on the device.
         ``spp_begin``/``spp_count``: one progressive pass (persistent engine,
         pixel seeding) -- see :meth:`trace_progressive`."""
+        if out is None:
+            ws = None
+        elif isinstance(wait_stream, str):
+            ws = _current_stream(self.device)
+        else:
+            ws = wait_stream
         d = _desc(width, height, spp, seed_mode, band_rows, shard, num_shards, engine,
                   (FLAG_COUNT_VISITS if count_visits else 0) | (FLAG_OUT_DEVICE if out is not None else 0),
-                  spp_begin, spp_count)
+                  spp_begin, spp_count, ws)
         rows = int(_tile_rows(ctypes.byref(d)))
         rays = ctypes.c_uint64()
         cam = camera._to_c()

@@ -2,9 +2,10 @@
 //   tmpt <width> <height> <spp> <objFile> [--seed row|pixel] [--engine persistent|wavefront|mega]
 //        [--gpus N] [--device D] [--out output.png]
 // Defaults reproduce the reference: row seeding (main.cpp:204) and output.png.
-// Pixel seeding is what the wavefront engine parallelises; row mode runs the
-// megakernel (one lane per row).  With --gpus N the rows are dealt to N
-// devices in 16-row bands, one host thread per device, and assembled here.
+// Pixel seeding is what the parallel engines need; row mode runs the
+// megakernel (one lane per row).  With --gpus N (tmpt_render_multi) the rows
+// are dealt round-robin one at a time (row y to device y % N), one host thread
+// per device, and the tiles are assembled into the frame.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>

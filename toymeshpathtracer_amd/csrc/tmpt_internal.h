@@ -123,6 +123,7 @@ struct Scene {
     float4* prog = nullptr;
     size_t prog_slots = 0;
     int32_t prog_key[7] = {0, 0, 0, 0, 0, 0, -1};
+    uint64_t prog_cam = 0;  // FNV-1a of the camera (and seed mode) of that pass
     int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
     // statistics of the last render
     double render_ms = 0.0;

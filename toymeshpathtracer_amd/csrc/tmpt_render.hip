@@ -1644,11 +1644,19 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     const bool progressive = a.smp_begin > 0 || a.smp_end < a.spp;
     if (progressive) {
         const int32_t key[6] = {d->width, d->height, d->spp, a.band_rows, a.shard, a.nshards};
+        // the carried colour sums and RNG states belong to one camera: a pass
+        // with another camera (or seeding) must not blend into them
+        uint64_t cam_key = 1469598103934665603ull;
+        const unsigned char* cb = reinterpret_cast<const unsigned char*>(cam);
+        for (size_t i = 0; i < sizeof(tmpt_camera); ++i) cam_key = (cam_key ^ cb[i]) * 1099511628211ull;
+        cam_key = (cam_key ^ (uint32_t)d->seed_mode) * 1099511628211ull;
         if (a.smp_begin > 0 &&
-            (memcmp(key, s.prog_key, sizeof(key)) != 0 || s.prog_key[6] != a.smp_begin)) {
-            set_error("tmpt_render: spp_begin does not continue the previous pass of this shard");
+            (memcmp(key, s.prog_key, sizeof(key)) != 0 || s.prog_key[6] != a.smp_begin || s.prog_cam != cam_key)) {
+            set_error("tmpt_render: spp_begin does not continue the previous pass of this shard "
+                      "(same camera, size, spp and shard)");
             return -22;
         }
+        s.prog_cam = cam_key;
         if (s.prog_slots < (size_t)a.slots) {
             if (s.prog) (void)hipFree(s.prog);
             s.prog = nullptr;
@@ -1659,6 +1667,17 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         a.prog = s.prog;
         memcpy(s.prog_key, key, sizeof(key));
         s.prog_key[6] = -1;  // valid again only once this pass completes
+    }
+    if (d->flags & TMPT_FLAG_WAIT_STREAM) {  // order after the caller's stream (tmpt.h)
+        hipEvent_t ev;
+        TMPT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(d->wait_stream)));
+        if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, ev, 0);
+        (void)hipEventDestroy(ev);
+        if (e != hipSuccess) {
+            set_error(std::string("tmpt_render: wait_stream: ") + hipGetErrorString(e));
+            return -1;
+        }
     }
     unsigned long long* d_counters = nullptr;
     constexpr int kCounters = 24;
