@@ -5,11 +5,18 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
 is launched by torch.distributed.run, one rank per GPU.  One *step* = one full
 frame of BASELINE.json configs[3]: sponza.obj 1920x1080, 64 spp (the
 deterministic stand-in scene, data/gen_standin_sponza.py; the real sponza.obj
-is absent from the reference), pixel-mode seeding, persistent path engine.  The frame
+is absent from the reference), sample seeding (below), persistent path engine.  The frame
 is sharded over the N GPUs in rows dealt round-robin (1-row bands; total work fixed:
 strong scaling); each rank renders its bands straight into a device tensor and
 one RCCL gather over xGMI assembles the image on rank 0 -- inside the timed
 region.  value = all rays of all ranks / max-over-ranks wall time.
+
+Seeding (--seed-mode): "sample" (default) = every pixel's own xorshift stream
+(seed (y*W+x)*9781+1, as pixel mode) with sample s starting 2^16*s steps into
+it, so a pixel's samples are independent work units; "pixel" = one stream per
+pixel, samples in sequence (the per-pixel chain bounds strong scaling).  Both
+are byte-exact against their oracle legs (tests/); the line also reports the
+other mode's throughput (seed_modes), timed the same way after the main run.
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
   roofline      dominant kernel (k_path: all queries of the frame): algorithmic
@@ -92,6 +99,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
     ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
+    ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel"])
+    ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding mode")
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
     ap.add_argument("--cpu-row-step", type=int, default=64, help="CPU baseline: every k-th row")
     ap.add_argument("--no-cpu", action="store_true")
@@ -120,6 +129,8 @@ def main() -> None:
     path = scene_path(obj)
     engine = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT,
               "mega": tm.ENGINE_MEGAKERNEL}[args.engine]
+    seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL}
+    seed = seeds[args.seed_mode]
     tris, bmin, bmax = tm.load_scene(path)
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
     t0 = time.perf_counter()
@@ -136,11 +147,11 @@ def main() -> None:
     gathered = [torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)] if rank == 0 else None
     image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
 
-    def step():
+    def step(seed=seed):
         # out= a device tile: the render waits for torch's current stream
         # (TMPT_FLAG_WAIT_STREAM), on which torch orders the previous step's
         # gather / assembly of the same tile, and returns once the tile is done
-        _, rays = scene.trace_image(cam, W, H, SPP, seed_mode=tm.SEED_PIXEL, engine=engine,
+        _, rays = scene.trace_image(cam, W, H, SPP, seed_mode=seed, engine=engine,
                                     band_rows=BAND_ROWS, shard=rank, num_shards=world,
                                     out=tile.data_ptr())
         st = scene.stats()
@@ -182,6 +193,33 @@ def main() -> None:
         rays = int(r.item())
 
     value = rays / elapsed / 1e6
+
+    # ---- the other seeding mode, timed the same way (reported, not `value`)
+    frame = image.cpu().numpy() if rank == 0 else None
+    compare = {}
+    if not args.no_compare:
+        for name, sd in seeds.items():
+            if sd == seed:
+                continue
+            step(sd)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            crays = sum(step(sd)[0] for _ in range(args.steps))
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            cel = time.perf_counter() - t1
+            if world > 1:
+                t = torch.tensor([cel], dtype=torch.float64, device=gdev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                cel = float(t.item())
+                r = torch.tensor([crays], dtype=torch.int64, device=gdev)
+                dist.all_reduce(r, op=dist.ReduceOp.SUM)
+                crays = int(r.item())
+            compare[name] = {"value": round(crays / cel / 1e6, 2), "ms_per_step": round(cel / args.steps * 1e3, 2),
+                             "rays_per_step": crays // args.steps}
     if rank != 0:
         scene.close()
         dist.destroy_process_group()
@@ -190,8 +228,7 @@ def main() -> None:
         log(f"gathered frame: {world} ranks ({args.dist_backend}), {rays} rays")
 
     # ---- roofline of the dominant kernel (extend), from an instrumented run
-    frame = image.cpu().numpy()
-    _, _ = scene.trace_image(cam, W, H, args.count_spp, seed_mode=tm.SEED_PIXEL, engine=engine,
+    _, _ = scene.trace_image(cam, W, H, args.count_spp, seed_mode=seed, engine=engine,
                              band_rows=BAND_ROWS, shard=rank, num_shards=world,
                              count_visits=True, out=tile.data_ptr())
     cs = scene.stats()
@@ -239,7 +276,8 @@ def main() -> None:
         threads = min(16, os.cpu_count() or 1)
         osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
         t1 = time.perf_counter()
-        ref, crays = osc.render(cam.as_array(), W, H, SPP, seed_mode=oracle.SEED_PIXEL,
+        ref, crays = osc.render(cam.as_array(), W, H, SPP,
+                                seed_mode={"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL}[args.seed_mode],
                                 row_step=args.cpu_row_step, threads=threads)
         cdt = time.perf_counter() - t1
         rows = np.arange(0, H, args.cpu_row_step)
@@ -252,7 +290,7 @@ def main() -> None:
         cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads,
                "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model,
                "sample": f"rows y%{args.cpu_row_step}==0 ({len(rows)} x {W} px x {SPP} spp, "
-                         f"{crays} rays, {cdt:.1f} s), octree restatement of scene.cpp, pixel seeding"}
+                         f"{crays} rays, {cdt:.1f} s), octree restatement of scene.cpp, {args.seed_mode} seeding"}
         diff = int((frame[rows] != ref[rows]).any(-1).sum())
         parity = {"rows_checked": int(len(rows)), "pixels_differ": diff,
                   "oracle": "octree (reference tie order)"}
@@ -298,9 +336,10 @@ def main() -> None:
                 "floor, data/gen_standin_sponza.py)" if sponza else "data/*.obj from the reference",
         "config": {"workload": f"{args.config}: {os.path.basename(path)} {W}x{H} {SPP}spp",
                    "global_batch": W * H, "spp": SPP, "tris": int(tris.shape[0]),
-                   "seed_mode": "pixel", "engine": args.engine,
+                   "seed_mode": args.seed_mode, "engine": args.engine,
                    "parallelism": f"row-bands{BAND_ROWS}x{world}",
                    "rays_per_step": rays // args.steps},
+        "seed_modes": compare,
         "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "host_paths": host,
         "scene_init_s": round(init_s, 3), "bvh_build_ms": round(st0.build_ms, 2),
         "bvh": {"lbvh2_depth": st0.bvh_depth, "bvh4_nodes": st0.bvh4_nodes, "bvh4_depth": st0.bvh4_depth,

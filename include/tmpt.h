@@ -24,7 +24,8 @@ extern "C" {
 
 #define TMPT_ABI_VERSION 5  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
                               4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
-                              progressive continuation keyed on the camera */
+                              progressive continuation keyed on the camera,
+                              TMPT_SEED_SAMPLE */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -34,7 +35,14 @@ typedef struct {
     float lens_radius;
 } tmpt_camera;
 
-enum { TMPT_SEED_ROW = 0, TMPT_SEED_PIXEL = 1 };
+/* RNG seeding of the xorshift32 stream (maths.cpp:5-13):
+ *   ROW    the reference: seed y*9781+1 per row, threaded along the row
+ *          (main.cpp:204) -- one lane per row
+ *   PIXEL  seed (y*W+x)*9781+1 per pixel (0 remapped), its samples in sequence
+ *   SAMPLE the pixel's seed as in PIXEL, sample s starting 2^16 * s steps into
+ *          that stream (a GF(2) jump), so the samples of a pixel are
+ *          independent work; the sum stays in sample order */
+enum { TMPT_SEED_ROW = 0, TMPT_SEED_PIXEL = 1, TMPT_SEED_SAMPLE = 2 };
 
 /* render engines */
 enum {
@@ -59,7 +67,7 @@ enum {
  * one band of the whole height. */
 typedef struct {
     int32_t width, height, spp;
-    int32_t seed_mode;  /* TMPT_SEED_ROW (main.cpp:204) or TMPT_SEED_PIXEL */
+    int32_t seed_mode;  /* TMPT_SEED_ROW (main.cpp:204), TMPT_SEED_PIXEL or TMPT_SEED_SAMPLE */
     int32_t band_rows;
     int32_t shard, num_shards;
     int32_t engine;
@@ -89,7 +97,8 @@ typedef struct {
  * stream, i.e. the stream the kernels are launched on). */
 typedef struct {
     double render_ms;             /* first kernel to last kernel of the call */
-    double extend_ms, shadow_ms;  /* summed closest-hit / any-hit kernel time */
+    double extend_ms, shadow_ms;  /* summed closest-hit / any-hit kernel time (persistent engine:
+                                     extend_ms = its k_path launches, both query kinds) */
     uint64_t extend_rays, shadow_rays;
     int64_t extend_launches, shadow_launches, iterations;
     uint64_t node_visits, tri_tests; /* extend (closest-hit) kernel, with TMPT_FLAG_COUNT_VISITS */

@@ -23,7 +23,8 @@ LIB = os.path.join(HERE, "build", "liboracle.so")
 
 ACCEL_OCTREE, ACCEL_BVH, ACCEL_LINEAR = 0, 1, 2
 TIE_VISIT, TIE_INDEX = 0, 1
-SEED_ROW, SEED_PIXEL = 0, 1
+SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
+SAMPLE_STRIDE = 65536  # xorshift steps between the starts of a pixel's samples (sample seeding)
 
 
 def build() -> None:
@@ -53,6 +54,7 @@ def _sig(name, res, args):
 
 _xorshift = _sig("orc_xorshift32", ctypes.c_uint32, [_u32p])
 _xorshift_jump = _sig("orc_xorshift32_jump", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64])
+_sample_seed = _sig("orc_sample_seed", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32])
 _rand01 = _sig("orc_random_float01", ctypes.c_float, [_u32p])
 _disk = _sig("orc_random_in_unit_disk", None, [_u32p, _f32p])
 _unitv = _sig("orc_random_unit_vector", None, [_u32p, _f32p])
@@ -93,6 +95,11 @@ def xorshift_seq(seed: int, n: int) -> np.ndarray:
 def xorshift_jump(seed: int, n: int) -> int:
     """State after n xorshift steps from `seed` (GF(2) matrix power, maths.cpp:5-13)."""
     return int(_xorshift_jump(seed, n))
+
+
+def sample_seed(seed: int, smp: int) -> int:
+    """Start state of sample `smp` in sample seeding: xorshift_jump(seed, smp * 2^16)."""
+    return int(_sample_seed(seed, smp))
 
 
 def float01_seq(seed: int, n: int) -> np.ndarray:

@@ -1,7 +1,7 @@
 /*
  * oracle_cli.c -- command-line driver for the CPU oracle (test infrastructure).
  * Mirrors main.cpp:248-345: <width> <height> <spp> <objfile>, plus options
- *   --seed row|pixel  --accel octree|bvh|linear  --tie visit|index
+ *   --seed row|pixel|sample  --accel octree|bvh|linear  --tie visit|index
  *   --threads N  --out file.rgba (raw RGBA, row 0 = bottom, as in memory)
  */
 #include "tmpt_oracle.h"
@@ -31,7 +31,10 @@ int main(int argc, char** argv)
     int threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     const char* out = NULL;
     for (int i = 5; i < argc; ++i) {
-        if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = !strcmp(argv[++i], "pixel");
+        if (!strcmp(argv[i], "--seed") && i + 1 < argc) {
+            ++i;
+            seed = !strcmp(argv[i], "pixel") ? ORC_SEED_PIXEL : (!strcmp(argv[i], "sample") ? ORC_SEED_SAMPLE : ORC_SEED_ROW);
+        }
         else if (!strcmp(argv[i], "--accel") && i + 1 < argc) {
             ++i;
             accel = !strcmp(argv[i], "bvh") ? ORC_ACCEL_BVH

@@ -69,8 +69,8 @@ uint32_t orc_xorshift32(uint32_t* state) /* maths.cpp:5-13 */
 /* Jump-ahead of the maths.cpp:5-13 xorshift by n steps (state after n calls).
  * One step is linear over GF(2)^32: x' = M x with M = (I+L15)(I+R17)(I+L13).
  * M^n by square-and-multiply on 32-column bit matrices (column j = image of
- * bit j).  Checker for the planned per-sample substream seeding mode
- * (DESIGN.md §6): sample s would start at M^(2^16 s) of the pixel seed. */
+ * bit j).  Sample seeding (ORC_SEED_SAMPLE): sample s starts at
+ * M^(2^16 s) of the pixel seed. */
 static uint32_t orc_gf2_apply(const uint32_t* m, uint32_t x)
 {
     uint32_t r = 0;
@@ -101,6 +101,27 @@ uint32_t orc_xorshift32_jump(uint32_t state, uint64_t n)
         n >>= 1;
     }
     return orc_gf2_apply(acc, state);
+}
+
+static void orc_jump_matrix(uint64_t n, uint32_t* acc) /* columns of M^n */
+{
+    uint32_t m[32];
+    for (int j = 0; j < 32; ++j) {
+        uint32_t x = 1u << j;
+        orc_xorshift32(&x);
+        m[j] = x;
+        acc[j] = 1u << j;
+    }
+    while (n) {
+        if (n & 1u) orc_gf2_mul(m, acc, acc);
+        orc_gf2_mul(m, m, m);
+        n >>= 1;
+    }
+}
+
+uint32_t orc_sample_seed(uint32_t seed, uint32_t smp)
+{
+    return orc_xorshift32_jump(seed, (uint64_t)smp * ORC_SAMPLE_STRIDE);
 }
 
 float orc_random_float01(uint32_t* state) /* maths.cpp:15-18 */
@@ -798,9 +819,13 @@ void orc_trace(const orc_scene* s, const float orig[3], const float dir[3], uint
     vstore(out_col, trace(s, vload(orig), vload(dir), rng, rays));
 }
 
-/* TraceImageBody::operator() for one row, main.cpp:192-238 */
+/* TraceImageBody::operator() for one row, main.cpp:192-238.  Seeding:
+ * row (main.cpp:204, the stream threads along the row), pixel (one stream per
+ * pixel, its samples in sequence) or sample (sample smp of the pixel starts at
+ * M^(smp * 2^16) of the pixel seed: jumps[smp] = that matrix's columns). */
 static uint64_t render_row(const orc_scene* s, const orc_camera* cam, int32_t w, int32_t h,
-                           int32_t spp, int32_t seed_mode, int64_t y, uint8_t* image)
+                           int32_t spp, int32_t seed_mode, int64_t y, uint8_t* image,
+                           const uint32_t* jumps)
 {
     const float invWidth = 1.0f / (float)w;     /* main.cpp:186 */
     const float invHeight = 1.0f / (float)h;    /* main.cpp:187 */
@@ -810,7 +835,9 @@ static uint64_t render_row(const orc_scene* s, const orc_camera* cam, int32_t w,
     for (int64_t x = 0; x < w; ++x) {
         if (seed_mode == ORC_SEED_PIXEL) rngState = orc_pixel_seed((int32_t)x, (int32_t)y, w);
         v3 col = V(0.0f, 0.0f, 0.0f);
+        const uint32_t pseed = orc_pixel_seed((int32_t)x, (int32_t)y, w);
         for (int64_t smp = 0; smp < spp; smp++) {
+            if (seed_mode == ORC_SEED_SAMPLE) rngState = orc_gf2_apply(jumps + 32 * smp, pseed);
             /* main.cpp:212-216, arguments sequenced left to right */
             float su = ((float)x + orc_random_float01(&rngState)) * invWidth;
             float sv = ((float)y + orc_random_float01(&rngState)) * invHeight;
@@ -836,6 +863,7 @@ typedef struct {
     const orc_camera* cam;
     int32_t w, h, spp, seed_mode, y0, y1, step;
     uint8_t* rgba;
+    const uint32_t* jumps;
     atomic_int next;
     atomic_ullong rays;
 } render_job;
@@ -848,7 +876,7 @@ static void* render_worker(void* arg)
         int k = atomic_fetch_add(&j->next, 1); /* grain size 1, main.cpp:329-331 */
         int64_t y = (int64_t)j->y0 + (int64_t)k * j->step;
         if (y >= j->y1) break;
-        local += render_row(j->s, j->cam, j->w, j->h, j->spp, j->seed_mode, y, j->rgba);
+        local += render_row(j->s, j->cam, j->w, j->h, j->spp, j->seed_mode, y, j->rgba, j->jumps);
     }
     atomic_fetch_add(&j->rays, local);
     return NULL;
@@ -861,6 +889,15 @@ uint64_t orc_render(const orc_scene* s, const orc_camera* cam, int32_t w, int32_
     render_job j;
     j.s = s; j.cam = cam; j.w = w; j.h = h; j.spp = spp; j.seed_mode = seed_mode;
     j.y0 = y0; j.y1 = y1 < h ? y1 : h; j.step = row_step > 0 ? row_step : 1; j.rgba = rgba;
+    uint32_t* jumps = NULL;
+    if (seed_mode == ORC_SEED_SAMPLE) { /* M^(smp * stride) for every sample index */
+        uint32_t stride[32];
+        jumps = (uint32_t*)malloc(sizeof(uint32_t) * 32 * (size_t)(spp > 0 ? spp : 1));
+        orc_jump_matrix(ORC_SAMPLE_STRIDE, stride);
+        for (int b = 0; b < 32; ++b) jumps[b] = 1u << b;
+        for (int32_t k = 1; k < spp; ++k) orc_gf2_mul(stride, jumps + 32 * (k - 1), jumps + 32 * k);
+    }
+    j.jumps = jumps;
     atomic_init(&j.next, 0);
     atomic_init(&j.rays, 0);
     if (nthreads < 1) nthreads = 1;
@@ -869,6 +906,7 @@ uint64_t orc_render(const orc_scene* s, const orc_camera* cam, int32_t w, int32_
     for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, render_worker, &j);
     render_worker(&j);
     for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
+    free(jumps);
     return atomic_load(&j.rays);
 }
 

@@ -42,11 +42,16 @@ enum { ORC_ACCEL_OCTREE = 0, ORC_ACCEL_BVH = 1, ORC_ACCEL_LINEAR = 2 };
  *   ORC_TIE_INDEX: lowest triangle index wins (= linear scan with strict '<') */
 enum { ORC_TIE_VISIT = 0, ORC_TIE_INDEX = 1 };
 /* RNG seeding: ROW = main.cpp:204 unmodified; PIXEL = per-pixel seed */
-enum { ORC_SEED_ROW = 0, ORC_SEED_PIXEL = 1 };
+enum { ORC_SEED_ROW = 0, ORC_SEED_PIXEL = 1, ORC_SEED_SAMPLE = 2 };
+/* sample seeding: sample s of a pixel starts ORC_SAMPLE_STRIDE xorshift steps per
+ * sample into the pixel's stream (state = M^(s * stride) * pixel seed) */
+#define ORC_SAMPLE_STRIDE 65536u
 
 /* ---- RNG / sampling KATs (maths.cpp:5-38) ---- */
 uint32_t orc_xorshift32(uint32_t* state);
 uint32_t orc_xorshift32_jump(uint32_t state, uint64_t n);
+/* start state of sample `smp` of the pixel whose pixel-mode seed is `seed` */
+uint32_t orc_sample_seed(uint32_t seed, uint32_t smp);
 float    orc_random_float01(uint32_t* state);
 void     orc_random_in_unit_disk(uint32_t* state, float out[3]);
 void     orc_random_unit_vector(uint32_t* state, float out[3]);

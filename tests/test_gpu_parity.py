@@ -558,3 +558,81 @@ def test_unit_sincos_device_matches_host_libm_every_key(gpu):
     ref = oracle.unit_sincos_range(0, n)
     bad = np.nonzero((dev.view(np.uint32) != ref.view(np.uint32)).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} keys differ, first {bad[:8]}"
+
+
+# ---------------------------------------------------------------- sample seeding
+@pytest.mark.parametrize("engine", [tm.ENGINE_PERSISTENT, tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+@pytest.mark.parametrize("name,w,h,spp", [("cube.obj", 320, 180, 4), ("suzanne.obj", 320, 180, 6),
+                                          ("teapot.obj", 160, 90, 5)])
+def test_sample_mode_matches_oracle(gpu, monkeypatch, engine, name, w, h, spp):
+    """TMPT_SEED_SAMPLE (sample s of a pixel starts 2^16*s steps into its
+    stream): byte-identical to the oracle's sample-seeded loop with every
+    block size of the persistent engine -- 1 sample per unit (per-sample
+    colours + in-order resolve), 2 and 4, and the whole pixel per unit."""
+    tris, bmin, bmax, sc = _scene(name)
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+    for blk in (["1", "2", "4", "1024"] if engine == tm.ENGINE_PERSISTENT else [None]):
+        if blk is not None:
+            monkeypatch.setenv("TMPT_SAMPLE_BLOCK", blk)
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, engine=engine)
+        assert rays == ref_rays, blk
+        diff = np.nonzero((img != ref).any(-1))
+        assert diff[0].size == 0, f"block {blk}: {diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+    sc.close()
+
+
+def test_sample_mode_shards_and_sizes(gpu, monkeypatch):
+    """Sample seeding: 1-row bands over 3 and 8 shards reassemble to the
+    1-shard frame with the same ray count (auto block size differs per
+    shard load: a property, not an oracle run), ragged sizes match the
+    oracle, and spp = 1 equals pixel mode."""
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    w, h, spp = 320, 180, 8
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
+    for n in (3, 8):
+        out = np.zeros_like(full)
+        total = 0
+        for k in range(n):
+            tile, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1, shard=k, num_shards=n)
+            out[tm.tile_row_to_y(w, h, 1, k, n)] = tile
+            total += r
+        assert np.array_equal(out, full) and total == rays, n
+    a, ra = sc.trace_image(cam, w, h, 1, seed_mode=tm.SEED_SAMPLE)
+    b, rb = sc.trace_image(cam, w, h, 1, seed_mode=tm.SEED_PIXEL)
+    assert ra == rb and np.array_equal(a, b)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    for (ww, hh, ss) in ((1, 1, 3), (65, 3, 7), (97, 33, 2)):
+        c2 = tm.Camera.for_scene(bmin, bmax, ww, hh)
+        img, r = sc.trace_image(c2, ww, hh, ss, seed_mode=tm.SEED_SAMPLE)
+        ref, rr = osc.render(c2.as_array(), ww, hh, ss, seed_mode=oracle.SEED_SAMPLE)
+        assert r == rr and np.array_equal(img, ref), (ww, hh, ss)
+    with pytest.raises(tm.TmptError, match="progressive"):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, spp_begin=0, spp_count=2)
+    sc.close()
+
+
+def test_sample_mode_bench_frame(gpu, sponza_path):
+    """The bench frame (stand-in sponza 1920x1080x64) in sample seeding: the
+    1/8 shard (the per-rank load at 8 GPUs) equals the same rows of the
+    single-GPU frame, ray counts add up, a row sample at 4 spp matches the
+    oracle, and a second render is identical (determinism)."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h = 1920, 1080
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris) as sc:
+        full, rays = sc.trace_image(cam, w, h, 64, seed_mode=tm.SEED_SAMPLE, band_rows=1)
+        tile, r0 = sc.trace_image(cam, w, h, 64, seed_mode=tm.SEED_SAMPLE, band_rows=1, shard=0, num_shards=8)
+        assert np.array_equal(tile, full[0::8])
+        rest = sum(sc.trace_image(cam, w, h, 64, seed_mode=tm.SEED_SAMPLE, band_rows=1, shard=k,
+                                  num_shards=8)[1] for k in range(1, 8))
+        assert r0 + rest == rays
+        small, _ = sc.trace_image(cam, w, h, 4, seed_mode=tm.SEED_SAMPLE)
+        small2, _ = sc.trace_image(cam, w, h, 4, seed_mode=tm.SEED_SAMPLE)
+    assert np.array_equal(small, small2)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, _ = osc.render(cam.as_array(), w, h, 4, seed_mode=oracle.SEED_SAMPLE, row_step=64)
+    rows = np.arange(0, h, 64)
+    assert np.array_equal(small[rows], ref[rows])

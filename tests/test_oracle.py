@@ -215,3 +215,72 @@ def test_pixel_rows_are_independent():
     part, _ = sc.render(cam, 160, 90, 2, seed_mode=oracle.SEED_PIXEL, y0=3, row_step=7)
     rows = np.arange(3, 90, 7)
     assert np.array_equal(part[rows], full[rows])
+
+
+# ---------------------------------------------------------------- sample seeding
+def _xorshift_np(x, n):
+    """n xorshift steps (maths.cpp:5-13) of every state in x, numpy, independent of the C oracle."""
+    x = x.astype(np.uint32).copy()
+    for _ in range(n):
+        x ^= x << np.uint32(13)
+        x ^= x >> np.uint32(17)
+        x ^= x << np.uint32(15)
+    return x
+
+
+def test_sample_seed_is_the_stream_at_sample_offsets():
+    """Sample seeding: sample s of a pixel starts 2^16 * s xorshift steps into
+    the pixel's own stream -- checked against sequential numpy steps."""
+    seeds = np.array([oracle.pixel_seed(x, y, 640) for x, y in ((0, 0), (5, 3), (639, 359), (100, 200))],
+                     np.uint32)
+    cur = seeds.copy()
+    for s in range(4):
+        assert [oracle.sample_seed(int(p), s) for p in seeds] == [int(v) for v in cur]
+        cur = _xorshift_np(cur, oracle.SAMPLE_STRIDE)
+    assert oracle.sample_seed(int(seeds[1]), 1000) == oracle.xorshift_jump(int(seeds[1]), 1000 * 2**16)
+
+
+def test_sample_mode_render_restated_from_primitives():
+    """The oracle's sample-seeded image loop (render_row with ORC_SEED_SAMPLE)
+    equals the loop of main.cpp:202-233 written out in Python over the oracle's
+    own pinned primitives, with each sample's stream started at its offset."""
+    tris, bmin, bmax = oracle.load_scene(data("suzanne.obj"))
+    w, h, spp = 12, 7, 3
+    cam = oracle.camera_for_scene(bmin, bmax, w, h)
+    sc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX)
+    img, rays = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+    inv_w, inv_h, recip = np.float32(1) / np.float32(w), np.float32(1) / np.float32(h), np.float32(1) / np.float32(spp)
+    ref = np.zeros((h, w, 4), np.uint8)
+    total = 0
+    for y in range(h):
+        for x in range(w):
+            col = np.zeros(3, np.float32)
+            for s in range(spp):
+                st = oracle.sample_seed(oracle.pixel_seed(x, y, w), s)
+                jx, jy = oracle.float01_seq(st, 2)
+                st = int(oracle.xorshift_seq(st, 2)[-1])
+                u = (np.float32(x) + jx) * inv_w
+                v = (np.float32(y) + jy) * inv_h
+                o, d, st = oracle.get_ray(cam, float(u), float(v), st)
+                c, st, r = sc.trace(o, d, st)
+                col = col + c
+                total += r
+            col = np.sqrt(col * recip)
+            ref[y, x, :3] = (np.minimum(np.maximum(col, 0), 1) * np.float32(255)).astype(np.uint8)
+            ref[y, x, 3] = 255
+    assert rays == total
+    assert np.array_equal(img, ref)
+
+
+def test_sample_mode_first_sample_is_pixel_mode():
+    """Sample 0 starts at the pixel seed: a 1-spp frame is the pixel-mode frame,
+    and with more samples the two modes differ (different streams)."""
+    tris, bmin, bmax = oracle.load_scene(data("cube.obj"))
+    cam = oracle.camera_for_scene(bmin, bmax, 80, 45)
+    sc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX)
+    a, ra = sc.render(cam, 80, 45, 1, seed_mode=oracle.SEED_SAMPLE)
+    b, rb = sc.render(cam, 80, 45, 1, seed_mode=oracle.SEED_PIXEL)
+    assert ra == rb and np.array_equal(a, b)
+    a, _ = sc.render(cam, 80, 45, 4, seed_mode=oracle.SEED_SAMPLE)
+    b, _ = sc.render(cam, 80, 45, 4, seed_mode=oracle.SEED_PIXEL)
+    assert not np.array_equal(a, b)

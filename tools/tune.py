@@ -21,7 +21,7 @@ import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
 BUILD_KEYS = ("TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
-RENDER_KEYS = ("TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
+RENDER_KEYS = ("TMPT_SAMPLE_BLOCK", "TMPT_SBUF", "TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
@@ -30,6 +30,7 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 scene_name = os.environ.get("TUNE_SCENE", "sponza")
 SHARDS = int(os.environ.get("TUNE_SHARDS", "1"))  # >1: render shard 0 of N (per-rank load at N GPUs)
 BAND = int(os.environ.get("TUNE_BAND", "16"))  # rows per band dealt round-robin to the shards
+SEED = {"pixel": tm.SEED_PIXEL, "sample": tm.SEED_SAMPLE}[os.environ.get("TUNE_SEED", "pixel")]
 W, H = 1920, 1080
 path = gen_standin_sponza.ensure() if scene_name == "sponza" else os.path.join(ROOT, "data", scene_name)
 tris, bmin, bmax = tm.load_scene(path)
@@ -73,7 +74,7 @@ for r in range(rounds):
             if env.get(k) is not None:
                 os.environ[k] = env[k]
         t0 = time.perf_counter()
-        img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_PIXEL, band_rows=BAND, shard=0,
+        img, rays = sc.trace_image(cam, W, H, spp, seed_mode=SEED, band_rows=BAND, shard=0,
                                    num_shards=SHARDS, engine=ENGINES[env.get("ENGINE", "persistent")])
         dt = time.perf_counter() - t0
         st = sc.stats()

@@ -28,11 +28,11 @@ import numpy as np
 
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
-    "SEED_ROW", "SEED_PIXEL", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
+    "SEED_ROW", "SEED_PIXEL", "SEED_SAMPLE", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
     "tile_rows", "tile_row_to_y", "render_multi",
 ]
 
-SEED_ROW, SEED_PIXEL = 0, 1
+SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
 ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL, ENGINE_PERSISTENT = 0, 1, 2
 FLAG_OUT_DEVICE, FLAG_COUNT_VISITS, FLAG_WAIT_STREAM = 1, 2, 4
 

@@ -199,10 +199,14 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.nodes4f) (void)hipFree(s.nodes4f);
     if (s.prog) (void)hipFree(s.prog);
+    if (s.jt) (void)hipFree(s.jt);
+    if (s.sbuf) (void)hipFree(s.sbuf);
     free_shadow_grid(s);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);
+    for (auto e : s.path_ev)
+        if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     delete h;
     return 0;
@@ -272,7 +276,7 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     if (d->width < 1 || d->width > 10000) return bad("tmpt_render: invalid width");
     if (d->height < 1 || d->height > 10000) return bad("tmpt_render: invalid height");
     if (d->spp < 1 || d->spp > 1024) return bad("tmpt_render: invalid samplesPerPixel");
-    if (d->seed_mode != TMPT_SEED_ROW && d->seed_mode != TMPT_SEED_PIXEL)
+    if (d->seed_mode != TMPT_SEED_ROW && d->seed_mode != TMPT_SEED_PIXEL && d->seed_mode != TMPT_SEED_SAMPLE)
         return bad("tmpt_render: invalid seed_mode");
     if (d->engine != TMPT_ENGINE_WAVEFRONT && d->engine != TMPT_ENGINE_MEGAKERNEL &&
         d->engine != TMPT_ENGINE_PERSISTENT)

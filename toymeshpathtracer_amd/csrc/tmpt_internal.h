@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "tmpt_math.h"
 
@@ -124,7 +125,14 @@ struct Scene {
     size_t prog_slots = 0;
     int32_t prog_key[7] = {0, 0, 0, 0, 0, 0, -1};
     uint64_t prog_cam = 0;  // FNV-1a of the camera (and seed mode) of that pass
+    // sample seeding: sample_seed's jump tables for samples [0, jt_spp), and the
+    // per-sample colour buffer of block-split pixels (tmpt_render.hip k_resolve)
+    uint32_t* jt = nullptr;
+    int32_t jt_spp = 0;
+    float4* sbuf = nullptr;
+    size_t sbuf_bytes = 0;
     int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
+    hipEvent_t path_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // around the pilot / final k_path
     // statistics of the last render
     double render_ms = 0.0;
     double extend_ms = 0.0;
@@ -150,6 +158,8 @@ const char* last_error();
 
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
+// tmpt_render.hip: sample_seed's byte tables for samples [0, spp) (1024 words each)
+void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab);
 // device radix sort of (key, value) pairs (tmpt_bvh.hip); returns 0 if the
 // result is in (keys, vals), 1 if in (tkeys, tvals)
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tkeys, uint32_t* tvals, int32_t n,

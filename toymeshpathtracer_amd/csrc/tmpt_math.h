@@ -156,6 +156,19 @@ TMPT_HD uint32_t pixel_seed(uint32_t x, uint32_t y, uint32_t w)
 }
 TMPT_HD uint32_t row_seed(uint32_t y) { return y * 9781u + 1u; }  // main.cpp:204
 
+// Sample seeding (TMPT_SEED_SAMPLE): sample s of a pixel starts
+// kSampleStride xorshift steps per sample into the pixel's own stream, so the
+// samples of a pixel are independent work.  xorshift32 is linear over
+// GF(2)^32, so the jump is the 32x32 bit matrix J_s = M^(s * kSampleStride),
+// applied through four byte tables: jt[s*1024 + 256k + b] = J_s (b << 8k).
+constexpr uint32_t kSampleStride = 65536u;
+TMPT_HD uint32_t sample_seed(const uint32_t* __restrict__ jt, uint32_t s, uint32_t seed)
+{
+    const uint32_t* t = jt + (size_t)s * 1024u;
+    return t[seed & 255u] ^ t[256u + ((seed >> 8) & 255u)] ^ t[512u + ((seed >> 16) & 255u)] ^
+           t[768u + (seed >> 24)];
+}
+
 // ---------------------------------------------------------------- camera
 // Field order of Camera, maths.h:106-111 (= tmpt_camera in include/tmpt.h).
 struct Camera {

@@ -38,6 +38,11 @@ struct RenderArgs {
     int32_t smp_begin, smp_end;
     float out_recip;  // 1/spp for the final pass, 1/smp_end for a preview
     float4* prog;
+    // sample seeding (TMPT_SEED_SAMPLE): jump tables of sample_seed (null in the
+    // other modes); a lane's run of samples ends where smp & bmask == 0 (its
+    // block of the persistent engine; 2047 = never inside 1..1024)
+    const uint32_t* jt;
+    uint32_t bmask;
 };
 
 __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
@@ -146,8 +151,10 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
                                                  TravCount& cnt)
 {
     f3 col = mk(0.0f, 0.0f, 0.0f);
+    const uint32_t pseed = rng;
     for (int s = 0; s < a.spp; ++s) {  // main.cpp:209-219
         f3 o, d;
+        if (a.jt) rng = sample_seed(a.jt, (uint32_t)s, pseed);  // sample seeding
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
         col = col + trace_path<WIDE, COUNT>(sv, o, d, rng, rays, st, lbuf, cnt);
     }
@@ -488,6 +495,7 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
                 int lr = (int)(p / (uint32_t)a.W), x = (int)(p - (uint32_t)lr * (uint32_t)a.W);
                 int y = tile_row_to_y(a, lr);
                 f3 o;
+                if (a.jt) rng = sample_seed(a.jt, smp, pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)a.W));
                 camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
                 s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
                 s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
@@ -579,6 +587,14 @@ struct PathCtl {
     uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
     uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
     uint32_t* __restrict__ tlog;  // PROF: per pixel {start, end (s_memrealtime), steps, shading rounds}
+    // Sample seeding: the supply hands out units = (pixel, block of blk
+    // samples), nblk blocks per pixel, unit u = pixel * nblk + block (P counts
+    // units).  With nblk > 1 each sample's colour goes to sbuf[s * slots + pixel]
+    // and k_resolve sums them in sample order (main.cpp:218's col += Trace).
+    uint32_t nblk, blk;
+    float4* __restrict__ sbuf;
+    uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp
+    int sb_nt;              // nontemporal stores
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -614,7 +630,7 @@ __device__ __forceinline__ uint2 simd_rank(uint32_t* reg)
 constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per block (7.5 KB)
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
-          int OCC = 1, int TAIL = 0, int PROF = 0, int HELP = 0>
+          int OCC = 1, int TAIL = 0, int PROF = 0, int HELP = 0, int SAMP = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -764,7 +780,14 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     take = min(take, pc.lane_cap - min(pc.lane_cap, (uint32_t)__popcll(wballot(has_pix))));
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
-                    pix = pc.order ? pc.order[res + k] : res + k;
+                    uint32_t smp0 = (uint32_t)a.smp_begin;
+                    if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
+                        const uint32_t unit = res + k;
+                        pix = unit / pc.nblk;
+                        smp0 = (unit - pix * pc.nblk) * pc.blk;
+                    } else {
+                        pix = pc.order ? pc.order[res + k] : res + k;
+                    }
                     psteps = 0;
                     if (PROF && pc.tlog) {
                         pt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -782,7 +805,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         col = mk(pv.x, pv.y, pv.z);
                         rng = __float_as_uint(pv.w);
                     }
-                    smp = (uint32_t)a.smp_begin;
+                    smp = smp0;
                     depth = 0;
                     if (COUNT) work0 = pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
                                                         : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
@@ -908,10 +931,20 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (!pend) {
                     for (int kk = (int)depth - 1; kk >= 0; --kk)
                         color = backward_step(color, light[kk * BLOCK]);
-                    col = col + color;
+                    if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve sums in sample order
+                        float4* dst = pc.sbuf + ((size_t)smp * pc.sb_ss + (size_t)pix * pc.sb_sp);
+                        const float4 v = make_float4(color.x, color.y, color.z, 0.0f);
+                        if (pc.sb_nt) {
+                            typedef float f32x4 __attribute__((ext_vector_type(4)));
+                            __builtin_nontemporal_store((f32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(dst));
+                        } else {
+                            *dst = v;
+                        }
+                    } else
+                        col = col + color;
                     ++smp;
                     depth = 0;
-                    if (smp < (uint32_t)a.smp_end) {
+                    if (smp < (uint32_t)a.smp_end && (!SAMP || (smp & a.bmask) != 0u)) {
                         cam = true;
                     } else {
                         if (a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
@@ -926,11 +959,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             pc.tlog[4 * (size_t)pix + 3] = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) |
                                                            (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu);
                         }
-                        out[pix] = (COUNT && pc.cost_map)
-                                       ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
-                                                           : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
-                                             work0
-                                       : pack_pixel(col, a.out_recip);
+                        if (!SAMP || !pc.sbuf)
+                            out[pix] = (COUNT && pc.cost_map)
+                                           ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
+                                                               : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
+                                                 work0
+                                           : pack_pixel(col, a.out_recip);
                         has_pix = false;
                     }
                 }
@@ -943,8 +977,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             if (cam) {  // next camera sample of this lane's pixel (main.cpp:212-216)
                 const int lr = (int)(pix / (uint32_t)a.W);
                 const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                camera_sample(a.cam, (uint32_t)x, (uint32_t)tile_row_to_y(a, lr), a.invW, a.invH, rng,
-                              so, sd);
+                const uint32_t y = (uint32_t)tile_row_to_y(a, lr);
+                if (SAMP) rng = sample_seed(a.jt, smp, pixel_seed((uint32_t)x, y, (uint32_t)a.W));
+                camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd);
                 start = true;
             }
             if (PROF >= 2) {
@@ -1096,6 +1131,23 @@ __global__ void __launch_bounds__(256) k_order_keys(const uint32_t* __restrict__
     vals[i] = (uint32_t)i;
 }
 
+// Sample seeding with several blocks per pixel: the pixel's colour is the sum
+// of its samples' colours in sample order (main.cpp:209-219, col += Trace),
+// then main.cpp:221-233.  sbuf is [sample][pixel]: coalesced reads.
+__global__ void __launch_bounds__(256) k_resolve(const float4* __restrict__ sbuf, int64_t P, int32_t spp,
+                                                  uint32_t ss, uint32_t sp, float spp_recip,
+                                                  uint32_t* __restrict__ out)
+{
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    for (int32_t s = 0; s < spp; ++s) {
+        const float4 c = sbuf[(size_t)s * ss + (size_t)p * sp];
+        col = col + mk(c.x, c.y, c.z);
+    }
+    out[p] = pack_pixel(col, spp_recip);
+}
+
 // ============================================================ host side
 namespace {
 
@@ -1134,6 +1186,54 @@ SceneView view(const Scene& s)
     return v;
 }
 
+// Columns of M^n, M the xorshift32 step as a GF(2) 32x32 matrix (maths.cpp:5-13):
+// column j = image of bit j.
+void gf2_mul(const uint32_t* x, const uint32_t* y, uint32_t* out)  // out = x * y
+{
+    uint32_t t[32];
+    for (int j = 0; j < 32; ++j) {
+        uint32_t r = 0;
+        for (int i = 0; i < 32; ++i)
+            if ((y[j] >> i) & 1u) r ^= x[i];
+        t[j] = r;
+    }
+    memcpy(out, t, sizeof t);
+}
+
+void xorshift_power(uint64_t n, uint32_t* acc)
+{
+    uint32_t m[32];
+    for (int j = 0; j < 32; ++j) {
+        uint32_t v = 1u << j;
+        m[j] = xorshift32(v);
+        acc[j] = 1u << j;
+    }
+    for (; n; n >>= 1) {
+        if (n & 1u) gf2_mul(m, acc, acc);
+        gf2_mul(m, m, m);
+    }
+}
+
+}  // namespace
+
+// sample_seed's byte tables for samples [0, spp): J_s = M^(s * kSampleStride)
+void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab)
+{
+    uint32_t stride[32], J[32];
+    xorshift_power(kSampleStride, stride);
+    for (int j = 0; j < 32; ++j) J[j] = 1u << j;
+    tab.assign((size_t)spp * 1024u, 0u);
+    for (int32_t smp = 0; smp < spp; ++smp) {
+        uint32_t* t = tab.data() + (size_t)smp * 1024u;
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 1; b < 256; ++b)  // table[b] = table[b without its lowest bit] ^ column
+                t[256 * k + b] = t[256 * k + (b & (b - 1u))] ^ J[8 * k + __builtin_ctz(b)];
+        gf2_mul(stride, J, J);
+    }
+}
+
+namespace {
+
 RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
 {
     RenderArgs a;
@@ -1161,6 +1261,8 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     a.smp_end = d->spp_count > 0 ? d->spp_begin + d->spp_count : d->spp;
     a.out_recip = a.smp_end == d->spp ? a.spp_recip : 1.0f / (float)a.smp_end;
     a.prog = nullptr;
+    a.jt = nullptr;
+    a.bmask = 2047u;
     return a;
 }
 
@@ -1378,6 +1480,10 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
 {
+    // HIP events around each k_path launch (pilot: 0-1, final: 2-3) on the
+    // stream it runs on: the dominant kernel's own time for the roofline
+    if (!s.path_ev[0])
+        for (auto& e : s.path_ev) TMPT_HIP(hipEventCreate(&e));
     // traversal rounds between shading checks / lanes waiting that trigger a
     // shading round (A/B on the bench frame at 1 and 8 shards, tools/tune.py)
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16;
@@ -1419,6 +1525,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 #undef TMPT_PV
         }
     }
+    if (a.jt)  // sample seeding: its own instantiation (the pixel-mode kernel keeps its registers)
+        fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>
+                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>;
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // TMPT_BLOCKS_PER_CU=<b> (A/B): fewer resident blocks than the occupancy allows
     if (const char* e = getenv("TMPT_BLOCKS_PER_CU")) {
@@ -1427,7 +1536,29 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             atoi(e) > 0)
             grid = std::min(grid, atoi(e) * cus);
     }
-    const int64_t P = a.slots;
+    // Sample seeding: the work units are (pixel, block of blk samples).  The
+    // block is the largest power of two that still leaves >= kUnitsPerLane
+    // units per resident lane (the frame's tail is then one block of the
+    // heaviest pixel, not its whole sample chain).  Bench frame (tools/tune.py,
+    // 1-row bands): N=1 blk 1/4/16/64 = 229.5/220.3/224.0/258.9 ms; 1/8 shard
+    // blk 1/2/4/8 = 29.4/29.4/30.2/32.7 ms.  96 picks 4 at N=1, 1 at 1/8.
+    // TMPT_SAMPLE_BLOCK=<b>.
+    uint32_t blk = 1u, nblk = 1u;
+    if (a.jt) {
+        constexpr int64_t kUnitsPerLane = 96;
+        const int64_t lanes0 = (int64_t)grid * kBlk;
+        blk = 1u;
+        while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)a.spp &&
+               a.slots * (((int64_t)a.spp + blk * 2 - 1) / (blk * 2)) >= kUnitsPerLane * lanes0)
+            blk *= 2u;
+        if (const char* e = getenv("TMPT_SAMPLE_BLOCK")) {
+            const int b = atoi(e);
+            if (b >= 1 && b <= 1024 && (b & (b - 1)) == 0) blk = (uint32_t)b;
+        }
+        while (a.slots * (((int64_t)a.spp + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
+        nblk = (uint32_t)(((int64_t)a.spp + blk - 1) / blk);
+    }
+    const int64_t P = a.slots * (int64_t)nblk;  // units the supply hands out
     // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
     // a shard has several pixels per resident lane, the frame ends with the
     // chains of the pixels started last.  A first pass runs kPilot samples of
@@ -1443,7 +1574,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     int pilot = 2 * P <= 5 * (int64_t)grid * kBlk ? 2 : 4, ratio10 = 0;
     if (const char* e = getenv("TMPT_PILOT")) pilot = std::max(0, atoi(e));
     if (const char* e = getenv("TMPT_PILOT_RATIO")) ratio10 = std::max(0, atoi(e));
-    const bool ordered = pilot > 0 && !count && a.smp_begin == 0 && a.smp_end == a.spp &&
+    const bool ordered = pilot > 0 && !count && !a.jt && a.smp_begin == 0 && a.smp_end == a.spp &&
                          a.spp >= 2 * pilot && 10 * P >= (int64_t)ratio10 * grid * kBlk && P < (1ll << 31);
     // Shadow offload at low load (k_path HELP): with at most ~2.5 pixels per
     // resident lane the frame is bound by the most expensive pixels' chains, and
@@ -1457,7 +1588,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // override the choice.
     const int64_t lanes = (int64_t)grid * kBlk;
     int help = ordered && fn == fn_default && fmt == 4 && 2 * P <= 5 * lanes ? 1 : 0;
-    if (const char* e = getenv("TMPT_HELP")) help = atoi(e) != 0 && !count && fmt == 4 && !prof;
+    if (const char* e = getenv("TMPT_HELP")) help = atoi(e) != 0 && !count && fmt == 4 && !prof && !a.jt;
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
     if (const char* e = getenv("TMPT_PAIR")) pair = atoi(e);
     if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 1>;
@@ -1487,6 +1618,36 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.dprio[0] = pc.dprio[1] = pc.dprio[2] = 0.0f;
     pc.dprio_cost = nullptr;
     pc.diag_noshadow = getenv("TMPT_DIAG_NOSHADOW") ? atoi(getenv("TMPT_DIAG_NOSHADOW")) : 0;
+    pc.nblk = nblk;
+    pc.blk = blk;
+    pc.sbuf = nullptr;
+    RenderArgs as = a;  // sample seeding: a lane's run of samples is its block
+    if (a.jt) {
+        as.bmask = nblk > 1 ? blk - 1u : 2047u;
+        if (nblk > 1) {
+            const size_t need = sizeof(float4) * (size_t)a.spp * (size_t)a.slots;
+            if (s.sbuf_bytes < need) {
+                if (s.sbuf) (void)hipFree(s.sbuf);
+                s.sbuf = nullptr;
+                s.sbuf_bytes = 0;
+                TMPT_HIP(hipMalloc(&s.sbuf, need));
+                s.sbuf_bytes = need;
+            }
+            pc.sbuf = s.sbuf;
+        }
+    }
+    // sbuf layout (TMPT_SBUF, A/B): 0 = [sample][pixel], 1 = [pixel][sample],
+    // 2 = [pixel][sample] with nontemporal stores
+    int sbl = 0;
+    if (const char* e = getenv("TMPT_SBUF")) sbl = atoi(e);
+    pc.sb_nt = sbl == 2;
+    if (sbl >= 1) {
+        pc.sb_ss = 1u;
+        pc.sb_sp = (uint32_t)a.spp;
+    } else {
+        pc.sb_ss = (uint32_t)a.slots;
+        pc.sb_sp = 1u;
+    }
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
     // slots and each wave's chain -- the frame's critical path at that load --
@@ -1512,8 +1673,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             TMPT_HIP(hipMemsetAsync(d_tlog, 0, (size_t)P * 16, s.stream));
         }
         pc.tlog = d_tlog;
+        TMPT_HIP(hipEventRecord(s.path_ev[2], s.stream));
         fn<<<grid, kBlk, 0, s.stream>>>(view(s), af, pc, d_out, (uint32_t*)s.ws, d_counters);
         TMPT_HIP(hipGetLastError());
+        TMPT_HIP(hipEventRecord(s.path_ev[3], s.stream));
         if (tl) {
             std::vector<uint32_t> h((size_t)P * 4);
             TMPT_HIP(hipStreamSynchronize(s.stream));
@@ -1527,7 +1690,12 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         return 0;
     };
     if (!ordered) {
-        if (final_launch(a)) return -1;
+        if (final_launch(as)) return -1;
+        if (pc.sbuf) {
+            k_resolve<<<(unsigned)((a.slots + 255) / 256), 256, 0, s.stream>>>(pc.sbuf, a.slots, a.spp, pc.sb_ss,
+                                                                             pc.sb_sp, a.spp_recip, d_out);
+            TMPT_HIP(hipGetLastError());
+        }
         s.path_launches = 1;
         return 0;
     }
@@ -1545,8 +1713,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     a1.out_recip = 1.0f / (float)pilot;
     a1.prog = state;
     pc.cost_out = cost;
+    TMPT_HIP(hipEventRecord(s.path_ev[0], s.stream));
     fn<<<grid, kBlk, 0, s.stream>>>(view(s), a1, pc, d_out, (uint32_t*)s.ws, d_counters);
     TMPT_HIP(hipGetLastError());
+    TMPT_HIP(hipEventRecord(s.path_ev[1], s.stream));
     k_order_keys<<<(unsigned)((P + 255) / 256), 256, 0, s.stream>>>(cost, a.W, a.tile_rows, keys, vals);
     const int which = radix_sort_pairs(keys, vals, tkeys, tvals, (int32_t)P, 16, hist, s.stream);
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
@@ -1668,6 +1838,23 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         memcpy(s.prog_key, key, sizeof(key));
         s.prog_key[6] = -1;  // valid again only once this pass completes
     }
+    if (a.seed_mode == TMPT_SEED_SAMPLE) {  // jump tables of sample_seed, grown to spp
+        if (s.jt_spp < a.spp) {
+            std::vector<uint32_t> tab;
+            sample_jump_tables(a.spp, tab);
+            uint32_t* nt = nullptr;
+            TMPT_HIP(hipMalloc(&nt, tab.size() * sizeof(uint32_t)));
+            if (hipMemcpy(nt, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipFree(nt);
+                set_error("tmpt_render: jump table upload failed");
+                return -1;
+            }
+            if (s.jt) (void)hipFree(s.jt);
+            s.jt = nt;
+            s.jt_spp = a.spp;
+        }
+        a.jt = s.jt;
+    }
     if (d->flags & TMPT_FLAG_WAIT_STREAM) {  // order after the caller's stream (tmpt.h)
         hipEvent_t ev;
         TMPT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1688,8 +1875,8 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     TMPT_HIP(hipEventCreate(&e1));
     TMPT_HIP(hipEventRecord(e0, s.stream));
     int rc = 0;
-    bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode == TMPT_SEED_PIXEL;
-    bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_PIXEL && use_wide();
+    bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode != TMPT_SEED_ROW;
+    bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode != TMPT_SEED_ROW && use_wide();
     if (progressive && !persistent) {
         set_error("tmpt_render: progressive spp needs the persistent engine (TMPT_BVH=2 is BVH2-only)");
         (void)hipEventDestroy(e0);
@@ -1724,7 +1911,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.render_ms = ms;
     if (progressive) s.prog_key[6] = a.smp_end < a.spp ? a.smp_end : -1;
     if (persistent) {  // one kernel for both query kinds
-        s.extend_ms = ms;
+        // k_path launches only (the render's other kernels: order keys, sort,
+        // resolve, memsets excluded)
+        float k1 = 0.0f, k0 = 0.0f;
+        (void)hipEventElapsedTime(&k1, s.path_ev[2], s.path_ev[3]);
+        if (s.path_launches == 2) (void)hipEventElapsedTime(&k0, s.path_ev[0], s.path_ev[1]);
+        s.extend_ms = (double)k0 + (double)k1;
         s.extend_rays = c[3];
         s.shadow_rays = c[0] - c[3];
         s.node_visits = c[1];
