@@ -636,3 +636,26 @@ def test_sample_mode_bench_frame(gpu, sponza_path):
     ref, _ = osc.render(cam.as_array(), w, h, 4, seed_mode=oracle.SEED_SAMPLE, row_step=64)
     rows = np.arange(0, h, 64)
     assert np.array_equal(small[rows], ref[rows])
+
+
+def test_cli_and_render_multi_sample_seeding(gpu, tmp_path):
+    """`tmpt ... --seed sample` writes the sample-seeded oracle's image, and
+    tmpt_render_multi (device repeated: two scenes, rows dealt round-robin,
+    one host thread each) assembles the same frame."""
+    import subprocess
+    from PIL import Image
+
+    cli = os.path.join(os.path.dirname(tm.lib_path), "tmpt")
+    out = tmp_path / "s.png"
+    w, h, spp = 200, 120, 3
+    r = subprocess.run([cli, str(w), str(h), str(spp), data("suzanne.obj"), "--seed", "sample", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    img = np.asarray(Image.open(out).convert("RGBA"))[::-1]  # back to row 0 = bottom
+    tris, bmin, bmax = tm.load_scene(data("suzanne.obj"))
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+    assert np.array_equal(img, ref)
+    multi, rays, _ = tm.render_multi(tris, cam, w, h, spp, [0, 0], seed_mode=tm.SEED_SAMPLE)
+    assert rays == ref_rays and np.array_equal(multi, ref)

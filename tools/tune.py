@@ -31,7 +31,7 @@ scene_name = os.environ.get("TUNE_SCENE", "sponza")
 SHARDS = int(os.environ.get("TUNE_SHARDS", "1"))  # >1: render shard 0 of N (per-rank load at N GPUs)
 BAND = int(os.environ.get("TUNE_BAND", "16"))  # rows per band dealt round-robin to the shards
 SEED = {"pixel": tm.SEED_PIXEL, "sample": tm.SEED_SAMPLE}[os.environ.get("TUNE_SEED", "pixel")]
-W, H = 1920, 1080
+W, H = map(int, os.environ.get("TUNE_RES", "1920x1080").split("x"))
 path = gen_standin_sponza.ensure() if scene_name == "sponza" else os.path.join(ROOT, "data", scene_name)
 tris, bmin, bmax = tm.load_scene(path)
 cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=scene_name == "sponza")

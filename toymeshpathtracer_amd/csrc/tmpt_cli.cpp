@@ -1,8 +1,8 @@
 // tmpt_cli.cpp -- the reference's command line (main.cpp:248-345) over the C ABI:
-//   tmpt <width> <height> <spp> <objFile> [--seed row|pixel] [--engine persistent|wavefront|mega]
+//   tmpt <width> <height> <spp> <objFile> [--seed row|pixel|sample] [--engine persistent|wavefront|mega]
 //        [--gpus N] [--device D] [--out output.png]
 // Defaults reproduce the reference: row seeding (main.cpp:204) and output.png.
-// Pixel seeding is what the parallel engines need; row mode runs the
+// Pixel or sample seeding is what the parallel engines need; row mode runs the
 // megakernel (one lane per row).  With --gpus N (tmpt_render_multi) the rows
 // are dealt round-robin one at a time (row y to device y % N), one host thread
 // per device, and the tiles are assembled into the frame.
@@ -24,7 +24,7 @@ static double now_s()
 int main(int argc, const char** argv)
 {
     if (argc < 5) {
-        printf("Usage: tmpt [width] [height] [samplesPerPixel] [objFile] [--seed row|pixel] "
+        printf("Usage: tmpt [width] [height] [samplesPerPixel] [objFile] [--seed row|pixel|sample] "
                "[--engine persistent|wavefront|mega] [--gpus N] [--device D] [--out file.png]\n");
         return 1;
     }
@@ -38,7 +38,11 @@ int main(int argc, const char** argv)
     int seed = TMPT_SEED_ROW, engine = TMPT_ENGINE_PERSISTENT, gpus = 1, device = 0;
     const char* out = "output.png";
     for (int i = 5; i < argc; ++i) {
-        if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strcmp(argv[++i], "pixel") ? TMPT_SEED_ROW : TMPT_SEED_PIXEL;
+        if (!strcmp(argv[i], "--seed") && i + 1 < argc) {
+            ++i;
+            seed = !strcmp(argv[i], "pixel") ? TMPT_SEED_PIXEL
+                                             : (!strcmp(argv[i], "sample") ? TMPT_SEED_SAMPLE : TMPT_SEED_ROW);
+        }
         else if (!strcmp(argv[i], "--engine") && i + 1 < argc) {
             ++i;
             engine = !strcmp(argv[i], "mega") ? TMPT_ENGINE_MEGAKERNEL

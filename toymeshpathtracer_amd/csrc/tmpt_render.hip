@@ -1525,9 +1525,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 #undef TMPT_PV
         }
     }
-    if (a.jt)  // sample seeding: its own instantiation (the pixel-mode kernel keeps its registers)
+    if (a.jt) {  // sample seeding: its own instantiation (the pixel-mode kernel keeps its registers)
         fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>
                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>;
+        if (prof)  // TMPT_PROF=1|2 (diagnostic): wave-time split of the sample kernel
+            fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2, 0, 1>
+                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1, 0, 1>;
+    }
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // TMPT_BLOCKS_PER_CU=<b> (A/B): fewer resident blocks than the occupancy allows
     if (const char* e = getenv("TMPT_BLOCKS_PER_CU")) {
