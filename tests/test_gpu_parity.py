@@ -659,3 +659,20 @@ def test_cli_and_render_multi_sample_seeding(gpu, tmp_path):
     assert np.array_equal(img, ref)
     multi, rays, _ = tm.render_multi(tris, cam, w, h, spp, [0, 0], seed_mode=tm.SEED_SAMPLE)
     assert rays == ref_rays and np.array_equal(multi, ref)
+
+
+def test_sample_mode_without_colour_buffer(gpu, monkeypatch):
+    """When the per-sample colour buffer would not fit (TMPT_SBUF_MAX stands in
+    for a frame too large for HBM), sample seeding runs whole pixels as units:
+    the same image and ray count."""
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    w, h, spp = 160, 90, 6
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    monkeypatch.setenv("TMPT_SAMPLE_BLOCK", "1")
+    a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
+    monkeypatch.setenv("TMPT_SBUF_MAX", "1024")
+    sc2 = tm.Scene(tris)  # no buffer held yet
+    b, rb = sc2.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
+    assert ra == rb and np.array_equal(a, b)
+    sc.close()
+    sc2.close()

@@ -834,11 +834,18 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (depth < (uint32_t)kMaxDepth) color = sky(r.d);
                 } else if (!qany) {  // closest hit (Trace, main.cpp:91-109)
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
-                        f3 pos, nrm;
-                        hit_record(sv, ts.best, ts.bu, ts.bv, pos, nrm);
+                        // the hit record's loads go out first; RandomUnitVector
+                        // (RNG + sincos, independent of them) runs while they are
+                        // in flight -- the same draws, the same values
+                        const float4* hp = reinterpret_cast<const float4*>(sv.tri_orig + ts.best);
+                        float4 ha = hp[0], hb = hp[1], hc = hp[2];
+                        f3 rnd = random_unit_vector(rng);
+                        materialize(ha, hb, hc);
+                        const f3 nrm = mk(hc.y, hc.z, hc.w);
+                        const f3 pos = hit_pos(mk(ha.x, ha.y, ha.z), mk(ha.w, hb.x, hb.y), mk(hb.z, hb.w, hc.x),
+                                               ts.bu, ts.bv);
                         const float lc = light_cosine(nrm, r.d);
                         light[depth * BLOCK] = lc;  // zeroed if occluded
-                        f3 rnd = random_unit_vector(rng);
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
@@ -1561,6 +1568,21 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
         while (a.slots * (((int64_t)a.spp + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
         nblk = (uint32_t)(((int64_t)a.spp + blk - 1) / blk);
+        // Several blocks per pixel need the per-sample colour buffer (16 B per
+        // sample of the tile: 2.1 GB at 1080p x 64).  If it does not fit in 3/4
+        // of the free device memory (or TMPT_SBUF_MAX bytes), the pixel is one
+        // unit: same image, only the tail of a small shard is longer.
+        if (nblk > 1) {
+            const size_t need = sizeof(float4) * (size_t)a.spp * (size_t)a.slots;
+            size_t fr = 0, tot = 0;
+            size_t budget = hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0;
+            budget += s.sbuf_bytes;  // the buffer already held is free for this call
+            if (const char* e = getenv("TMPT_SBUF_MAX")) budget = std::min(budget, (size_t)strtoull(e, nullptr, 10));
+            if (need > budget) {
+                while (blk < (uint32_t)a.spp) blk *= 2u;
+                nblk = 1u;
+            }
+        }
     }
     const int64_t P = a.slots * (int64_t)nblk;  // units the supply hands out
     // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
