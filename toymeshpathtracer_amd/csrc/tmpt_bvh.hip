@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
         int e = (int)ceil(log2(fmax(ext, 1e-30) / 255.0));
         e = max(-126, min(127, e));
         scale[a] = ldexp(1.0, e);
-        ebits |= (uint32_t)(e + 127) << (8 * a);
+        ebits |= ((uint32_t)e & 0xFFu) << (8 * a);  // signed byte: scale = 2^e (ldexp in the traversal)
     }
     // empty slots: inverted quantised box (lo 255 > hi 0) and a link to the null
     // leaf, so a step that does not consult the mask still finds nothing there

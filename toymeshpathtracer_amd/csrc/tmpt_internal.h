@@ -31,7 +31,7 @@ static_assert(sizeof(BvhNode) == 64, "node is one half cache line");
 // 4-wide node with quantised child boxes (DESIGN.md "BVH4Q"): 64 B, one
 // half cache line, 4 x dwordx4 loads for FOUR child boxes.
 //   a: origin.xyz (node box min, f32), w = exponents ex,ey,ez (bytes 0-2,
-//      biased by 127: scale = 2^(e-127)) | child-valid mask (byte 3)
+//      signed: scale = 2^e) | child-valid mask (byte 3)
 //   b: qlo.x[4], qhi.x[4], qlo.y[4], qhi.y[4]   (uint8 per child, child k in byte k)
 //   c: qlo.z[4], qhi.z[4], 0, 0
 //   d: child links: >=0 node index; <0 leaf = 0x80000000 | (count-1)<<27 | first slot

@@ -211,7 +211,14 @@ __device__ __forceinline__ bool trav_step(const SceneView& sv, const TravRay& r,
     return false;
 }
 
-__device__ __forceinline__ float exp_scale(uint32_t biased) { return __uint_as_float((biased & 0xFFu) << 23); }
+// 2^e for the signed exponent byte e of a BVH4Q node (bits 0-7 of `b`)
+__device__ __forceinline__ float exp_scale(uint32_t b) { return __uint_as_float((uint32_t)((int)(int8_t)(b & 0xFFu) + 127) << 23); }
+// x * 2^e for the signed exponent byte e at bit `sh` of w: v_bfe_i32 + v_ldexp_f32,
+// exact (a power-of-two scaling, no under/overflow for the 1/d of a unit direction)
+__device__ __forceinline__ float exp_mul(float x, uint32_t w, int sh)
+{
+    return __builtin_amdgcn_ldexpf(x, (int)__builtin_amdgcn_sbfe(w, sh, 8));
+}
 
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool leaf_tris(const SceneView& sv, const TravRay& r, float tmin,
@@ -513,8 +520,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             L = make_int4((int)l4.x, (int)l4.y, (int)l4.z, (int)l4.w);
         }
         if (COUNT) ++cnt.nodes;
-        const float sx = exp_scale(A.w) * r.ix, sy = exp_scale(A.w >> 8) * r.iy,
-                    sz = exp_scale(A.w >> 16) * r.iz;
+        const float sx = exp_mul(r.ix, A.w, 0), sy = exp_mul(r.iy, A.w, 8), sz = exp_mul(r.iz, A.w, 16);
         const float bx = __builtin_fmaf(__uint_as_float(A.x), r.ix, -r.ox);
         const float by = __builtin_fmaf(__uint_as_float(A.y), r.iy, -r.oy);
         const float bz = __builtin_fmaf(__uint_as_float(A.z), r.iz, -r.oz);
