@@ -1533,11 +1533,26 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
     }
     if (a.jt) {  // sample seeding: its own instantiation (the pixel-mode kernel keeps its registers)
-        fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>
-                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 1>;
+        // sparse-wave divisor 2 (shade once half of the lanes still holding work
+        // wait, when fewer than 32 hold any): bench frame 220.4 -> 218.2 ms at N=1,
+        // 29.4 -> 29.0 ms at the 1/8 shard (TMPT_TUNE=902 sweep)
+        constexpr int kSparseS = 2;
+        fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>
+                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>;
         if (prof)  // TMPT_PROF=1|2 (diagnostic): wave-time split of the sample kernel
-            fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2, 0, 1>
-                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1, 0, 1>;
+            fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 2, 0, 1>
+                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 1, 0, 1>;
+        // TMPT_TUNE=902,<steps>,<shade_min>,<sparse>: round-cadence variants of the sample kernel (A/B)
+        if (const char* tune = getenv("TMPT_TUNE")) {
+            int t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+            if (sscanf(tune, "%d,%d,%d,%d", &t0, &t1, &t2, &t3) == 4 && t0 == 902 && !count) {
+#define TMPT_SV(ST_, SM_, SP_) \
+    if (t1 == ST_ && t2 == SM_ && t3 == SP_) fn = k_path<false, kBlk, kPathSL, ST_, SM_, 1, 4, 4, SP_, 0, 0, 1>;
+                TMPT_SV(16, 16, 4) TMPT_SV(16, 16, 2) TMPT_SV(16, 16, 1) TMPT_SV(16, 16, 3) TMPT_SV(16, 20, 2)
+                TMPT_SV(20, 20, 2) TMPT_SV(20, 16, 2) TMPT_SV(16, 24, 2) TMPT_SV(16, 24, 1) TMPT_SV(16, 32, 1)
+#undef TMPT_SV
+            }
+        }
     }
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // TMPT_BLOCKS_PER_CU=<b> (A/B): fewer resident blocks than the occupancy allows
