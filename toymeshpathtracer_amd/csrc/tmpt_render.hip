@@ -1566,12 +1566,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // block is the largest power of two that still leaves >= kUnitsPerLane
     // units per resident lane (the frame's tail is then one block of the
     // heaviest pixel, not its whole sample chain).  Bench frame (tools/tune.py,
-    // 1-row bands): N=1 blk 1/4/16/64 = 229.5/220.3/224.0/258.9 ms; 1/8 shard
-    // blk 1/2/4/8 = 29.4/29.4/30.2/32.7 ms.  96 picks 4 at N=1, 1 at 1/8.
-    // TMPT_SAMPLE_BLOCK=<b>.
+    // 1-row bands, k_path ms): N=1 blk 2/4/8 = 220.7/217.8/217.3; 1/2 shard
+    // blk 1/2/4/8 = 113.3/110.9/110.2/111.7; 1/4 blk 1/2/4 = 57.1/56.2/56.6;
+    // 1/8 blk 1/2/4/8 = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane, so
+    // 60 picks 8, 4, 2, 1 at N = 1, 2, 4, 8.  TMPT_SAMPLE_BLOCK=<b>.
     uint32_t blk = 1u, nblk = 1u;
     if (a.jt) {
-        constexpr int64_t kUnitsPerLane = 96;
+        constexpr int64_t kUnitsPerLane = 60;
         const int64_t lanes0 = (int64_t)grid * kBlk;
         blk = 1u;
         while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)a.spp &&
