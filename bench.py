@@ -101,6 +101,9 @@ def main() -> None:
     ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
     ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel"])
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding mode")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the collective path (process group, gather, max-over-ranks) even at one rank "
+                         "(tests the RCCL calls on a 1-GPU box)")
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
     ap.add_argument("--cpu-row-step", type=int, default=64, help="CPU baseline: every k-th row")
     ap.add_argument("--no-cpu", action="store_true")
@@ -115,11 +118,12 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    dist_on = world > 1 or args.force_dist  # the collective path (process group, gather, reductions)
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1) if args.dist_backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
-    if world > 1:
+    if dist_on:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
         else:
@@ -142,7 +146,7 @@ def main() -> None:
     max_rows = max(len(r) for r in rows_of)
     my_rows = len(rows_of[rank])
     tile = torch.zeros((max_rows, W, 4), dtype=torch.uint8, device=dev)
-    gloo = world > 1 and args.dist_backend == "gloo"
+    gloo = dist_on and args.dist_backend == "gloo"
     gdev = torch.device("cpu") if gloo else dev
     gathered = [torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)] if rank == 0 else None
     image = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
@@ -155,16 +159,16 @@ def main() -> None:
                                     band_rows=BAND_ROWS, shard=rank, num_shards=world,
                                     out=tile.data_ptr())
         st = scene.stats()
-        if world > 1:
+        if dist_on:
             dist.gather(tile.cpu() if gloo else tile, gathered, dst=0)
         if rank == 0:  # de-interleave the bands into the frame, on the device
-            parts = [g.to(dev) for g in gathered] if gloo else (gathered if world > 1 else [tile])
+            parts = [g.to(dev) for g in gathered] if gloo else (gathered if dist_on else [tile])
             sharding.assemble(parts, rows_of, image)
         return rays, st
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -181,10 +185,10 @@ def main() -> None:
         sh_rays += st.shadow_rays
         ext_launches += st.extend_launches
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -202,16 +206,16 @@ def main() -> None:
             if sd == seed:
                 continue
             step(sd)
-            if world > 1:
+            if dist_on:
                 dist.barrier()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             crays = sum(step(sd)[0] for _ in range(args.steps))
             torch.cuda.synchronize()
-            if world > 1:
+            if dist_on:
                 dist.barrier()
             cel = time.perf_counter() - t1
-            if world > 1:
+            if dist_on:
                 t = torch.tensor([cel], dtype=torch.float64, device=gdev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 cel = float(t.item())
@@ -224,7 +228,7 @@ def main() -> None:
         scene.close()
         dist.destroy_process_group()
         return
-    if world > 1:
+    if dist_on:
         log(f"gathered frame: {world} ranks ({args.dist_backend}), {rays} rays")
 
     # ---- roofline of the dominant kernel (extend), from an instrumented run
@@ -348,7 +352,7 @@ def main() -> None:
     }
     print(json.dumps(out), flush=True)
     scene.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

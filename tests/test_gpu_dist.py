@@ -47,3 +47,22 @@ def test_bench_two_ranks_gloo_matches_single(gpu, tmp_path):
     a = np.asarray(Image.open(one).convert("RGBA"))
     b = np.asarray(Image.open(two).convert("RGBA"))
     assert np.array_equal(a, b)
+
+
+def test_bench_rccl_path_one_rank(gpu, tmp_path):
+    """The nccl (= RCCL) calls of bench.py's N>1 step -- process group on the
+    device, gather of the device tile, device-side max/sum reductions,
+    barriers -- run on the box's one GPU with --force-dist at world size 1
+    (RCCL refuses two ranks on one device); the frame must equal the plain
+    single-process frame."""
+    one = tmp_path / "one.png"
+    rccl = tmp_path / "rccl.png"
+    common = ["--config", "teapot720", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-compare"]
+    r1 = _bench(["bench.py", "--gpus", "1", "--save", str(one)] + common)
+    port = _free_port()
+    r2 = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+                 "--master-port", str(port), "bench.py", "--gpus", "1", "--force-dist", "--save", str(rccl)] + common)
+    assert r2["n_gpus"] == 1 and r2["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
+    a = np.asarray(Image.open(one).convert("RGBA"))
+    b = np.asarray(Image.open(rccl).convert("RGBA"))
+    assert np.array_equal(a, b)
