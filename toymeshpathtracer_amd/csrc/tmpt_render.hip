@@ -1155,6 +1155,32 @@ __global__ void __launch_bounds__(256) k_resolve(const float4* __restrict__ sbuf
     out[p] = pack_pixel(col, spp_recip);
 }
 
+// The same over a [pixel][sample] buffer: one wave per 64 pixels stages 16
+// samples of each in LDS with coalesced 256-B reads (16 lanes per pixel run),
+// then every lane sums its own pixel's samples in order.
+__global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sbuf, int64_t P, int32_t spp,
+                                                    float spp_recip, uint32_t* __restrict__ out)
+{
+    constexpr int kC = 16;                  // samples per staged chunk
+    __shared__ float4 tile[64][kC + 1];     // +1: a lane's row starts on another bank
+    const int64_t p0 = (int64_t)blockIdx.x * 64;
+    const int t = threadIdx.x;
+    const int np = (int)min<int64_t>(64, P - p0);
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    for (int32_t s0 = 0; s0 < spp; s0 += kC) {
+        const int nc = min(kC, spp - s0);
+        for (int e = t; e < 64 * kC; e += 64) {
+            const int i = e / kC, j = e - i * kC;
+            if (i < np && j < nc) tile[i][j] = sbuf[(size_t)(p0 + i) * (size_t)spp + (size_t)(s0 + j)];
+        }
+        __syncthreads();
+        if (t < np)
+            for (int j = 0; j < nc; ++j) col = col + mk(tile[t][j].x, tile[t][j].y, tile[t][j].z);
+        __syncthreads();
+    }
+    if (t < np) out[p0 + t] = pack_pixel(col, spp_recip);
+}
+
 // ============================================================ host side
 namespace {
 
@@ -1679,8 +1705,11 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
     }
     // sbuf layout (TMPT_SBUF, A/B): 0 = [sample][pixel], 1 = [pixel][sample],
-    // 2 = [pixel][sample] with nontemporal stores
-    int sbl = 0;
+    // 2 = [pixel][sample] with nontemporal stores (default: a 16-B store into
+    // [sample][pixel] pulls its whole line into L2 -- 27 GB of extra fetches
+    // per 1080p frame -- while nontemporal stores of a pixel's runs do not;
+    // k_resolve_px reads the pixel-major buffer through LDS)
+    int sbl = 2;
     if (const char* e = getenv("TMPT_SBUF")) sbl = atoi(e);
     pc.sb_nt = sbl == 2;
     if (sbl >= 1) {
@@ -1734,8 +1763,12 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     if (!ordered) {
         if (final_launch(as)) return -1;
         if (pc.sbuf) {
-            k_resolve<<<(unsigned)((a.slots + 255) / 256), 256, 0, s.stream>>>(pc.sbuf, a.slots, a.spp, pc.sb_ss,
-                                                                             pc.sb_sp, a.spp_recip, d_out);
+            if (pc.sb_ss == 1u)
+                k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(pc.sbuf, a.slots, a.spp,
+                                                                                 a.spp_recip, d_out);
+            else
+                k_resolve<<<(unsigned)((a.slots + 255) / 256), 256, 0, s.stream>>>(pc.sbuf, a.slots, a.spp, pc.sb_ss,
+                                                                                 pc.sb_sp, a.spp_recip, d_out);
             TMPT_HIP(hipGetLastError());
         }
         s.path_launches = 1;
