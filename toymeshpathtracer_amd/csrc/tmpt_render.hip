@@ -1527,7 +1527,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const char* nf = getenv("TMPT_NODE");
     const char nc = nf ? nf[0] : 't';
     const int fmt = nc == 'q' ? 0 : (nc == 'f' ? 1 : (nc == 's' ? 2 : (nc == 'n' ? 3 : 4)));
-    constexpr int kSparse = 4;  // sparse-wave shading threshold divisor (k_path TAIL)
+    // sparse-wave shading threshold divisor (k_path TAIL): 2 -- bench frame,
+    // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms)
+    constexpr int kSparse = 2;
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
     PathFn fn = nullptr;
 #define TMPT_PF(C_, F_) \
@@ -1535,6 +1537,14 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3) TMPT_PF(true, 4)
     TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3) TMPT_PF(false, 4)
 #undef TMPT_PF
+    // TMPT_TUNE=903,<sparse>: the pixel-mode kernel with another sparse-wave divisor (A/B)
+    if (const char* tune = getenv("TMPT_TUNE")) {
+        int t0 = 0, t1 = 0;
+        if (sscanf(tune, "%d,%d", &t0, &t1) == 2 && t0 == 903 && !count && fmt == 4) {
+            if (t1 == 4) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, 4>;
+            if (t1 == 1) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, 1>;
+        }
+    }
     const PathFn fn_default = fn;
     // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
     const char* pe = getenv("TMPT_PROF");
@@ -1562,7 +1572,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         // sparse-wave divisor 2 (shade once half of the lanes still holding work
         // wait, when fewer than 32 hold any): bench frame 220.4 -> 218.2 ms at N=1,
         // 29.4 -> 29.0 ms at the 1/8 shard (TMPT_TUNE=902 sweep)
-        constexpr int kSparseS = 2;
+        constexpr int kSparseS = kSparse;
         fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>
                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>;
         if (prof)  // TMPT_PROF=1|2 (diagnostic): wave-time split of the sample kernel
