@@ -81,6 +81,33 @@ def test_hitscene_kat(gpu, name):
     sc.close()
 
 
+@pytest.mark.parametrize("env", [{"TMPT_BUILDER": "lbvh"}, {"TMPT_COLLAPSE": "sah"}, {"TMPT_LEAF_MAX": "4"},
+                                 {"TMPT_TREELET": "3"}, {"TMPT_TREELET": "1", "TMPT_TREELET_MIN": "64"},
+                                 {"TMPT_LAYOUT": "1"}, {"TMPT_TREELET": "2", "TMPT_LAYOUT": "1"}])
+def test_build_variants_match_oracle(gpu, monkeypatch, env):
+    """Every build option (LBVH builder, SAH collapse, leaf size, treelet
+    restructuring, sibling-block node layout) changes the tree, never the
+    answers: HitScene on 200k rays and a sample-seeded frame equal the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    rays = _random_rays(tris, 200_000, seed=13)
+    ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    oids, ohits = osc.hit_batch(rays, 0.001, 1.0e7)
+    assert (ids >= 0).sum() > 1000 and np.array_equal(ids, oids)
+    h = ids >= 0
+    assert np.array_equal(hits[h].view(np.uint32), ohits[h].view(np.uint32))
+    aids, _ = sc.hit_scene_batch(rays, 0.001, 1.0e7, any_hit=True)
+    assert np.array_equal(aids >= 0, ids >= 0)
+    w, hh, spp = 160, 90, 4
+    cam = tm.Camera.for_scene(bmin, bmax, w, hh)
+    img, nrays = sc.trace_image(cam, w, hh, spp, seed_mode=tm.SEED_SAMPLE)
+    ref, ref_rays = osc.render(cam.as_array(), w, hh, spp, seed_mode=oracle.SEED_SAMPLE)
+    assert nrays == ref_rays and np.array_equal(img, ref)
+    sc.close()
+
+
 @pytest.mark.parametrize("name", ["cube.obj", "suzanne.obj"])
 def test_hitscene_vs_linear_scan(gpu, name):
     """Against the brute-force linear scan (the upstream algorithm)."""

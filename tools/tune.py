@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-BUILD_KEYS = ("TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
+BUILD_KEYS = ("TMPT_TREELET", "TMPT_TREELET_MIN", "TMPT_LAYOUT", "TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
 RENDER_KEYS = ("TMPT_SAMPLE_BLOCK", "TMPT_SBUF", "TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
@@ -59,6 +59,11 @@ def scene_for(env):
         st = sc.stats()
         print(f"scene {dict(key)}: build {st.build_ms:.1f} ms, bvh4 nodes {st.bvh4_nodes}, depth4 "
               f"{st.bvh4_depth}, ploc iters {st.builder_iters}", flush=True)
+        if os.environ.get("TUNE_COUNT"):  # node visits / triangle tests per query (4 spp)
+            _, q = sc.trace_image(cam, W, H, 4, seed_mode=SEED, band_rows=BAND, count_visits=True)
+            cs = sc.stats()
+            print(f"  visits per query at 4 spp: nodes {(cs.node_visits + cs.shadow_node_visits) / q:.3f}, "
+                  f"tris {(cs.tri_tests + cs.shadow_tri_tests) / q:.3f} ({q} queries)", flush=True)
         scenes[key] = sc
     return scenes[key]
 

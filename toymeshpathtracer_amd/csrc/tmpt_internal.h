@@ -58,6 +58,7 @@ static_assert(sizeof(Bvh4FNode) == 128, "BVH4F node is one 128-B line");
 constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
+constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per path block (7.5 KB)
 
 // Light-space grid for the shadow query (tmpt_shadow.hip): R x R cells over
 // the plane orthogonal to the light direction, per cell the triangles whose

@@ -627,7 +627,6 @@ __device__ __forceinline__ uint2 simd_rank(uint32_t* reg)
     return make_uint2((uint32_t)__shfl((int)r, 0), (uint32_t)__shfl((int)d, 0));
 }
 
-constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per block (7.5 KB)
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
           int OCC = 1, int TAIL = 0, int PROF = 0, int HELP = 0, int SAMP = 0>
