@@ -43,6 +43,9 @@ struct RenderArgs {
     // block of the persistent engine; 2047 = never inside 1..1024)
     const uint32_t* jt;
     uint32_t bmask;
+    // row seeding in the megakernel: rows per wave (lanes 0..row_lanes-1 each
+    // run one row's chain; the rest of the wave idles)
+    int32_t row_lanes;
 };
 
 __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
@@ -175,8 +178,11 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
     uint32_t rays = 0;
     TravCount cnt;
     const int64_t items = ROW ? (int64_t)a.tile_rows : a.slots;
-    const int64_t stride = (int64_t)gridDim.x * BLOCK;
-    for (int64_t w = gtid; w < items; w += stride) {
+    // ROW: lane l < row_lanes of wave v takes rows v*row_lanes + l, strided
+    // over the grid's waves (one chain per lane, spread over the SIMDs)
+    const int64_t first = ROW ? (lane_id() < a.row_lanes ? (gtid >> 6) * a.row_lanes + lane_id() : items) : gtid;
+    const int64_t stride = ROW ? (int64_t)gridDim.x * (BLOCK / 64) * a.row_lanes : (int64_t)gridDim.x * BLOCK;
+    for (int64_t w = first; w < items; w += stride) {
         if (ROW) {
             int lr = (int)w;
             int y = tile_row_to_y(a, lr);
@@ -1295,6 +1301,8 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     a.prog = nullptr;
     a.jt = nullptr;
     a.bmask = 2047u;
+    a.row_lanes = 1;  // one row per wave: measured fastest
+    if (const char* e = getenv("TMPT_ROW_LANES")) a.row_lanes = std::max(1, std::min(64, atoi(e)));
     return a;
 }
 
@@ -1303,7 +1311,8 @@ int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long
 {
     auto fn = k_mega<WIDE, ROW, COUNT, kBlk, kSL>;
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
-    int64_t items = ROW ? a.tile_rows : a.slots;
+    // ROW: one wave per row_lanes rows (up to the resident grid)
+    int64_t items = ROW ? ((int64_t)a.tile_rows + a.row_lanes - 1) / a.row_lanes * 64 : a.slots;
     grid = (int)std::min<int64_t>(grid, (items + kBlk - 1) / kBlk);
     grid = std::max(grid, 1);
     size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);
