@@ -110,7 +110,27 @@ __device__ __forceinline__ void flush_counts(unsigned long long* counters, uint3
 }
 
 // ============================================================ megakernel
-template <bool WIDE, bool COUNT, int BLOCK, int SL>
+// Whole query; Q2: the persistent engine's step (octant decode, top nodes from
+// the block's LDS copy), for the latency-bound row chains.
+template <bool WIDE, bool ANY, bool COUNT, bool Q2, int BLOCK, int SL>
+__device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float& t, float& u, float& v,
+                                          TravStack<BLOCK, SL>& st, TravCount& cnt)
+{
+    if (!Q2) return traverse<WIDE, ANY, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+    TravState ts;
+    trav_init(ts, kMaxT);
+    if (sv.n > 0 && !ray_has_nan(o, d)) {
+        const TravRay r = make_trav_ray(o, d);
+        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, 1, true>(sv, r, ANY, ts, st, cnt)) {
+        }
+    }
+    t = ts.bt;
+    u = ts.bu;
+    v = ts.bv;
+    return ts.best;
+}
+
+template <bool WIDE, bool COUNT, int BLOCK, int SL, bool Q2 = false>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
                                          TravCount& cnt)
@@ -120,7 +140,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
         ++rays;
         float t, u, v;
-        int id = traverse<WIDE, false, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+        int id = mega_query<WIDE, false, COUNT, Q2>(sv, o, d, t, u, v, st, cnt);
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
@@ -128,8 +148,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
             float lc = light_cosine(nrm, d);
             if (lc > 0.0f) {  // a zero light term does not depend on the answer
                 float ts, us, vs;
-                int sid = traverse<WIDE, true, COUNT>(sv, make_trav_ray(pos, light_dir()), kMinT, kMaxT,
-                                                      ts, us, vs, st, cnt);
+                int sid = mega_query<WIDE, true, COUNT, Q2>(sv, pos, light_dir(), ts, us, vs, st, cnt);
                 if (sid >= 0) lc = 0.0f;
             }
             lbuf[depth * BLOCK] = lc;
@@ -147,7 +166,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     return color;
 }
 
-template <bool WIDE, bool COUNT, int BLOCK, int SL>
+template <bool WIDE, bool COUNT, int BLOCK, int SL, bool Q2 = false>
 __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const RenderArgs& a, int x,
                                                  int y, uint32_t& rng, uint32_t& rays,
                                                  TravStack<BLOCK, SL>& st, float* lbuf,
@@ -159,7 +178,7 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
         f3 o, d;
         if (a.jt) rng = sample_seed(a.jt, (uint32_t)s, pseed);  // sample seeding
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-        col = col + trace_path<WIDE, COUNT>(sv, o, d, rng, rays, st, lbuf, cnt);
+        col = col + trace_path<WIDE, COUNT, BLOCK, SL, Q2>(sv, o, d, rng, rays, st, lbuf, cnt);
     }
     return pack_pixel(col, a.spp_recip);
 }
@@ -175,6 +194,18 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     float* lbuf = &s_light[threadIdx.x];
+    // ROW (one latency-bound chain per wave): the persistent engine's node step,
+    // with the top BVH4 levels copied to LDS
+    constexpr bool Q2 = ROW && WIDE;
+    if (Q2) {
+        __shared__ uint4 s_top[Q2 ? kTopNodes * 4 : 1];
+        const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
+        const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
+        for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
+        __syncthreads();
+        st.top = (const lds_u4*)s_top;
+        st.ntop = ntop;
+    }
     uint32_t rays = 0;
     TravCount cnt;
     const int64_t items = ROW ? (int64_t)a.tile_rows : a.slots;
@@ -188,7 +219,7 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
             int y = tile_row_to_y(a, lr);
             uint32_t rng = row_seed((uint32_t)y);  // main.cpp:204, unmodified
             for (int x = 0; x < a.W; ++x)
-                out[(int64_t)lr * a.W + x] = render_pixel<WIDE, COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+                out[(int64_t)lr * a.W + x] = render_pixel<WIDE, COUNT, BLOCK, SL, Q2>(sv, a, x, y, rng, rays, st, lbuf, cnt);
         } else {
             int lr = (int)(w / a.W), x = (int)(w - (int64_t)lr * a.W);
             int y = tile_row_to_y(a, lr);
