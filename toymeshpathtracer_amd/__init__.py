@@ -37,7 +37,8 @@ ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL, ENGINE_PERSISTENT = 0, 1, 2
 FLAG_OUT_DEVICE, FLAG_COUNT_VISITS, FLAG_WAIT_STREAM = 1, 2, 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "_lib", "libtmpt.so")
+# TMPT_LIB_PATH: another in-tree build of the library (compiler-flag A/B in tools/)
+lib_path = os.environ.get("TMPT_LIB_PATH") or os.path.join(_HERE, "_lib", "libtmpt.so")
 
 
 class TmptError(RuntimeError):
