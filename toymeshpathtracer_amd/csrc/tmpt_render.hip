@@ -1081,7 +1081,19 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (!vote || !leaf_round) { ++rs_nr; rs_nl += (uint64_t)__popcll(at_node); }
                 if (!vote || leaf_round) { ++rs_lr; rs_ll += (uint64_t)__popcll(at_leaf); }
             }
-            if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
+            if (FMT == 4 && !COUNT && vote) {
+                // voted round: the kind is wave-uniform, so only its code runs
+                // (a scalar branch instead of exec-mask splits around both)
+                const bool stepping = in_query && ((ts.node < 0) == leaf_round);
+                bool done = false;
+                if (leaf_round) {
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, 1, true, 2>(sv, r, qany, ts, st, cnt);
+                } else {
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, 1, true, 1>(sv, r, qany, ts, st, cnt);
+                }
+                if (done) in_query = false;
+                if (stepping && (pc.cost_out || pc.tlog || dp0 > 0.0f)) ++psteps;
+            } else if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
                 if (COUNT) {
                     TravCount c1;
                     if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, c1)) in_query = false;

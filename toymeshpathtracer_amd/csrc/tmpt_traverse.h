@@ -497,12 +497,14 @@ __device__ __forceinline__ bool trav_step4f_mixed(const SceneView& sv, const Tra
 // child pairs, no per-child min/max and no mask test (empty slots carry an
 // inverted box and link to the null leaf).  4 loads per node (the TA cost of a
 // divergent gather scales with bytes per lane) at ~BVH4F's VALU count.
-template <bool COUNT, int BLOCK, int SL, int SORTK = 0, bool TOPC = false>
+template <bool COUNT, int BLOCK, int SL, int SORTK = 0, bool TOPC = false, int KIND = 0>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt)
 {
-    if (ts.node >= 0) {
+    // KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a
+    // voted round), so the other kind's code is not emitted at all
+    if (KIND == 1 || (KIND == 0 && ts.node >= 0)) {
         // 32-bit byte offset off an SGPR base: one VALU for the address
         uint4 A, B, C;
         int4 L;
@@ -586,7 +588,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                 return false;
             }
         }
-    } else {
+    }
+    if (KIND == 2 || (KIND == 0 && ts.node < 0)) {
         const uint32_t code = (uint32_t)ts.node;
         const uint32_t first = code & kLeafFirstMask;
         const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
