@@ -628,6 +628,13 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             const float4* p = reinterpret_cast<const float4*>(base + (first + k) * (uint32_t)sizeof(TriPre));
             if (tri(p[0], p[1], p[2])) return true;
         }
+        if (KIND == 2 && ts.sp <= SL) {  // branch-free pop from the LDS part
+            const uint32_t top = st.lds[(uint32_t)max(ts.sp - 1, 0) * BLOCK];
+            const bool done = ts.sp == 0;
+            ts.node = (int)top;
+            ts.sp -= done ? 0 : 1;
+            return done;
+        }
     }
     if (ts.sp == 0) return true;
     ts.node = st.pop(ts.sp);
