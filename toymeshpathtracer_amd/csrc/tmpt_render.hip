@@ -1070,10 +1070,19 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             continue;
         }
         for (int k = 0; k < STEPS; ++k) {  // traversal rounds
-            const uint64_t at_leaf = wballot(in_query && ts.node < 0);
-            const uint64_t at_node = wballot(in_query && ts.node >= 0);
-            if ((at_leaf | at_node) == 0) break;
-            const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
+            // two compares straight to lane masks (a ballot of a combined bool
+            // made the compiler materialise it in a VGPR and compare again)
+            const uint64_t q = wballot(in_query);
+            const uint64_t at_leaf = q & wballot(ts.node < 0);
+            const uint64_t at_node = q & ~at_leaf;
+            if (q == 0) break;
+            // 32-bit counts, so the vote stays a scalar compare (the 64-bit
+            // popcount compare was widened onto the VALU)
+            const uint32_t n_leaf = (uint32_t)__builtin_popcount((uint32_t)at_leaf) +
+                                    (uint32_t)__builtin_popcount((uint32_t)(at_leaf >> 32));
+            const uint32_t n_node = (uint32_t)__builtin_popcount((uint32_t)at_node) +
+                                    (uint32_t)__builtin_popcount((uint32_t)(at_node >> 32));
+            const bool leaf_round = n_leaf > n_node;
             // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds
             // (latency of the few remaining pixels over lane efficiency)
             const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
