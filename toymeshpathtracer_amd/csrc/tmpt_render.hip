@@ -692,8 +692,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         st.top = (const lds_u4*)s_top;
         st.ntop = ntop;
     }
-    float dp0 = pc.dprio[0], dp1 = pc.dprio[1], dp2 = pc.dprio[2];
-    if (pc.dprio_cost && pc.order && a.smp_begin > 0) {  // relative thresholds (wave-uniform)
+    // SAMP: the sample kernel has none of pixel mode's pilot order, balanced
+    // first chunks, priorities, progressive state, trace log or shadow grid
+    // (answers without the grid are the same); compiling them out frees the
+    // scalar registers they held
+    constexpr bool kFull = !SAMP;
+    float dp0 = kFull ? pc.dprio[0] : 0.0f, dp1 = kFull ? pc.dprio[1] : 0.0f, dp2 = kFull ? pc.dprio[2] : 0.0f;
+    if (kFull && pc.dprio_cost && pc.order && a.smp_begin > 0) {  // relative thresholds (wave-uniform)
         const float sc = (float)pc.dprio_cost[pc.order[0]] * (float)(a.smp_end - a.smp_begin) / (float)a.smp_begin;
         dp0 *= sc;
         dp1 *= sc;
@@ -706,7 +711,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
     uint32_t res = 0, res_end = 0;
     bool exhausted = pc.P == 0;
-    if (pc.simd_reg && !exhausted) {  // SIMD-balanced first chunk
+    if (kFull && pc.simd_reg && !exhausted) {  // SIMD-balanced first chunk
         const uint2 rd = simd_rank(pc.simd_reg);
         if (rd.x < pc.wps && rd.y < pc.nsimd) {
             const uint32_t c = rd.x * pc.nsimd + ((rd.x & 1u) ? pc.nsimd - 1u - rd.y : rd.y);
@@ -791,7 +796,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         if (lane_id() == 0) b = atomicAdd(&pc.heads[seg * kCtr], 1u);
                         b = (uint32_t)__shfl((int)b, 0);
                     }
-                    if (b < c && pc.claim) {  // taken as some wave's balanced first chunk?
+                    if (b < c && kFull && pc.claim) {  // taken as some wave's balanced first chunk?
                         uint32_t got = 0;
                         if (lane_id() == 0) got = atomicExch(&pc.claim[seg + b * (uint32_t)kSeg], 1u) == 0u;
                         if (!__shfl((int)got, 0)) continue;
@@ -799,7 +804,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (b < c) {
                         res = (seg + b * (uint32_t)kSeg) * pc.chunk;
                         res_end = (uint32_t)min<int64_t>((int64_t)res + pc.chunk, pc.P);
-                        if (pc.prio_q != 0) {  // issue priority by cost rank (wave-uniform)
+                        if (kFull && pc.prio_q != 0) {  // issue priority by cost rank (wave-uniform)
                             const uint32_t q = res / pc.prio_q;
                             if (q == 0) __builtin_amdgcn_s_setprio(3);
                             else if (q == 1) __builtin_amdgcn_s_setprio(2);
@@ -822,18 +827,18 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         pix = unit / pc.nblk;
                         smp0 = (unit - pix * pc.nblk) * pc.blk;
                     } else {
-                        pix = pc.order ? pc.order[res + k] : res + k;
+                        pix = (kFull && pc.order) ? pc.order[res + k] : res + k;
                     }
                     psteps = 0;
-                    if (PROF && pc.tlog) {
+                    if (PROF && kFull && pc.tlog) {
                         pt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         pnsh = 0;
                     }
-                    if (!PROF && pc.tlog) pc.tlog[4 * (size_t)pix] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                    if (!PROF && kFull && pc.tlog) pc.tlog[4 * (size_t)pix] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                    if (a.smp_begin == 0) {
+                    if (!kFull || a.smp_begin == 0) {
                         rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
                         col = mk(0.0f, 0.0f, 0.0f);
                     } else {  // progressive: continue the previous pass's stream and sum
@@ -886,12 +891,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 nd = normalize(target - pos);
                         ++depth;
                         bool traced = false;
-                        if (lc > 0.0f && !pc.diag_noshadow) {
+                        if (lc > 0.0f && !(kFull && pc.diag_noshadow)) {
                             // shadow query: with the light-space grid, the triangles of
                             // the origin's cell (one leaf range, tested by the leaf
                             // steps of the traversal rounds); without, the BVH
-                            if (sv.sg.R > 0) gcell = shadow_grid_cell(sv, pos);
-                            if (sv.sg.R == 0 || gcell.y != 0) {
+                            const bool grid = kFull && sv.sg.R > 0;
+                            if (grid) gcell = shadow_grid_cell(sv, pos);
+                            if (!grid || gcell.y != 0) {
                                 nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
                                 nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
                                 start = true;  // shadow query toward the light
@@ -899,7 +905,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                                 so = pos;
                                 sd = ldir;
                                 traced = true;
-                                want_off = HELP != 0 && sv.sg.R == 0;
+                                want_off = HELP != 0 && !grid;
                             }
                         }
                         if (!traced) {  // nothing to trace (no light term, or an empty cell)
@@ -990,12 +996,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (smp < (uint32_t)a.smp_end && (!SAMP || (smp & a.bmask) != 0u)) {
                         cam = true;
                     } else {
-                        if (a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
-                        if (pc.cost_out) pc.cost_out[pix] = psteps;
-                        if (PROF && pc.tlog)
+                        if (kFull && a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
+                        if (kFull && pc.cost_out) pc.cost_out[pix] = psteps;
+                        if (PROF && kFull && pc.tlog)
                             *reinterpret_cast<uint4*>(&pc.tlog[4 * (size_t)pix]) =
                                 make_uint4(pt0, (uint32_t)__builtin_amdgcn_s_memrealtime(), psteps, pnsh);
-                        if (!PROF && pc.tlog) {  // start was stored at the fetch
+                        if (!PROF && kFull && pc.tlog) {  // start was stored at the fetch
                             pc.tlog[4 * (size_t)pix + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                             pc.tlog[4 * (size_t)pix + 2] = psteps;
                             // where it ran: XCC_ID << 16 | HW_ID[15:0] (wave, SIMD, CU, SH, SE)
@@ -1101,7 +1107,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, 1, true, 1>(sv, r, qany, ts, st, cnt);
                 }
                 if (done) in_query = false;
-                if (stepping && (pc.cost_out || pc.tlog || dp0 > 0.0f)) ++psteps;
+                if (stepping && ((kFull && (pc.cost_out || pc.tlog)) || dp0 > 0.0f)) ++psteps;
             } else if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
                 if (COUNT) {
                     TravCount c1;
@@ -1112,7 +1118,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
                     in_query = false;
                 }
-                if (pc.cost_out || pc.tlog || dp0 > 0.0f) ++psteps;
+                if ((kFull && (pc.cost_out || pc.tlog)) || dp0 > 0.0f) ++psteps;
             }
             if (PROF) {
                 const uint64_t t = stamp();
