@@ -215,6 +215,29 @@ TMPT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tMin, float tMax, fl
     return t >= tMin && t <= tMax;
 }
 
+// The same test without early exits: every quantity is computed and the
+// four rejections of maths.cpp:345-371 are combined at the end. Each value is
+// the same expression of the same inputs, so an accepted hit has the same
+// bits, and a rejected one is rejected (NaNs fail the final t range test as
+// they fail the reference's). For wave64 code, where a divergent early exit
+// saves nothing unless the whole wave leaves.
+TMPT_HD bool mt_test_flat(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tMin, float tMax, float& t, float& u,
+                          float& v)
+{
+    const f3 pvec = cross(d, e2);
+    const float det = dot(e1, pvec);
+    const float invDet = 1.0f / det;
+    const f3 tvec = o - v0;
+    u = dot(tvec, pvec) * invDet;
+    const f3 qvec = cross(tvec, e1);
+    v = dot(d, qvec) * invDet;
+    t = dot(e2, qvec) * invDet;
+    const bool small = det > -kDetEps && det < kDetEps;
+    const bool out_u = u < 0.0f || u > 1.0f;
+    const bool out_v = v < 0.0f || u + v > 1.0f;
+    return !small && !out_u && !out_v && t >= tMin && t <= tMax;
+}
+
 // Hit record of the accepted triangle, maths.cpp:375-377.
 TMPT_HD f3 hit_pos(f3 v0, f3 v1, f3 v2, float u, float v)
 {

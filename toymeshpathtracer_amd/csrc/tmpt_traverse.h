@@ -622,8 +622,33 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         float4 a1 = p1[0], b1 = p1[1], c1 = p1[2];
         materialize(a0, b0, c0);
         materialize(a1, b1, c1);
-        if (tri(a0, b0, c0)) return true;
-        if (n > 1u && tri(a1, b1, c1)) return true;
+        if (KIND == 2) {
+            // both tests without early exits, then the closest-hit order
+            // (triangle 0 first; an any-hit query stops at the first accept)
+            float t0, u0, w0, t1, u1, w1;
+            if (COUNT) cnt.tris += n > 1u ? 2u : 1u;
+            const bool ok0 = mt_test_flat(r.o, r.d, mk(a0.x, a0.y, a0.z), mk(a0.w, b0.x, b0.y),
+                                          mk(b0.z, b0.w, c0.x), kMinT, kMaxT, t0, u0, w0);
+            const bool ok1 = mt_test_flat(r.o, r.d, mk(a1.x, a1.y, a1.z), mk(a1.w, b1.x, b1.y),
+                                          mk(b1.z, b1.w, c1.x), kMinT, kMaxT, t1, u1, w1) &&
+                             n > 1u;
+            const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
+            const bool acc0 = ok0 && (t0 < ts.bt || (t0 == ts.bt && ts.best >= 0 && id0 < ts.best));
+            ts.bt = acc0 ? t0 : ts.bt;
+            ts.bu = acc0 ? u0 : ts.bu;
+            ts.bv = acc0 ? w0 : ts.bv;
+            ts.best = acc0 ? id0 : ts.best;
+            const bool acc1 = ok1 && !(any && acc0) &&
+                              (t1 < ts.bt || (t1 == ts.bt && ts.best >= 0 && id1 < ts.best));
+            ts.bt = acc1 ? t1 : ts.bt;
+            ts.bu = acc1 ? u1 : ts.bu;
+            ts.bv = acc1 ? w1 : ts.bv;
+            ts.best = acc1 ? id1 : ts.best;
+            if (any && (acc0 || acc1)) return true;
+        } else {
+            if (tri(a0, b0, c0)) return true;
+            if (n > 1u && tri(a1, b1, c1)) return true;
+        }
         for (uint32_t k = 2; k < n; ++k) {
             const float4* p = reinterpret_cast<const float4*>(base + (first + k) * (uint32_t)sizeof(TriPre));
             if (tri(p[0], p[1], p[2])) return true;
