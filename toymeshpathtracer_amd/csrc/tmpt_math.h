@@ -113,27 +113,25 @@ TMPT_HD uint32_t glibc_abstop12(float f) { return (__builtin_bit_cast(uint32_t, 
 
 TMPT_HD void glibc_sincosf_unit(float a, float& c, float& s)
 {
+    // One path for every angle, no branches: for 0 <= a < pi/4 the reduction
+    // gives n = 0 and xr = a exactly (fma(-0, pi/2, x) = x), so it evaluates
+    // glibc's |a| < pi/4 polynomials; for a < 2^-12 those round to glibc's
+    // sin = a, cos = 1 (the terms beyond x and 1 are below half an ulp).
+    // Both polynomials are evaluated once and swapped by quadrant parity.
+    // All 2^24 keys are checked against the host libm (tests/test_host.py)
+    // and on the device (tests/test_gpu_parity.py).
     const double x = a;
-    if (glibc_abstop12(a) < glibc_abstop12(0x1.921FB6p-1f)) {  // |a| < pi/4
-        if (glibc_abstop12(a) < glibc_abstop12(0x1p-12f)) {
-            s = a;
-            c = 1.0f;
-            return;
-        }
-        const double x2 = x * x;
-        s = glibc_sincosf_poly(x, x2, false, 0);
-        c = glibc_sincosf_poly(x, x2, false, 1);
-        return;
-    }
-    // reduce_fast: r = a * (2/pi * 2^24), n = (int(r) + 2^23) >> 24
     const double r = x * 0x1.45F306DC9C883p+23;
     const int n = ((int32_t)r + 0x800000) >> 24;
     const double xr = __builtin_fma(-(double)n, 0x1.921FB54442D18p0, x);
     const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -xr : xr;  // sign[n & 3] = {1, -1, -1, 1}
     const double x2 = xr * xr;
     const bool neg = (n & 2) != 0;
-    s = glibc_sincosf_poly(xs, x2, neg, n);
-    c = glibc_sincosf_poly(xs, x2, neg, n ^ 1);
+    const float ps = glibc_sincosf_poly(xs, x2, neg, 0);  // sine polynomial
+    const float pc = glibc_sincosf_poly(xs, x2, neg, 1);  // cosine polynomial
+    const bool odd = (n & 1) != 0;
+    s = odd ? pc : ps;
+    c = odd ? ps : pc;
 }
 
 // RandomUnitVector, maths.cpp:30-38 (cosf/sinf of the host libm, above).

@@ -623,7 +623,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         materialize(a0, b0, c0);
         materialize(a1, b1, c1);
         if (KIND == 2) {
-            // both tests without early exits, then the closest-hit order
+            // voted leaf round: both tests without early exits (the two
+            // dependency chains interleave), then the closest-hit order
             // (triangle 0 first; an any-hit query stops at the first accept)
             float t0, u0, w0, t1, u1, w1;
             if (COUNT) cnt.tris += n > 1u ? 2u : 1u;
@@ -645,7 +646,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             ts.bv = acc1 ? w1 : ts.bv;
             ts.best = acc1 ? id1 : ts.best;
             if (any && (acc0 || acc1)) return true;
-        } else {
+        } else {  // a lone lane (row chains) gains more from the early exits
             if (tri(a0, b0, c0)) return true;
             if (n > 1u && tri(a1, b1, c1)) return true;
         }
