@@ -744,6 +744,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     bool helper = false, waiting = false;
     uint32_t hown = 0;  // helper: owner lane << 4 | light slot
     uint32_t pix = 0, rng = 0, smp = 0, depth = 0;
+    // SAMP: the four jump-table words of the next sample's seed, loaded one
+    // camera phase ahead (pf_smp = the sample they belong to), so a new sample
+    // does not wait for their memory round trip
+    uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf_smp = 0xFFFFFFFFu, pf_pix = 0;
     uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
     uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
     uint32_t pt0 = 0, pnsh = 0;  // PROF + tlog: pixel start time, shading rounds while held
@@ -1027,7 +1031,20 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const int lr = (int)(pix / (uint32_t)a.W);
                 const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
                 const uint32_t y = (uint32_t)tile_row_to_y(a, lr);
-                if (SAMP) rng = sample_seed(a.jt, smp, pixel_seed((uint32_t)x, y, (uint32_t)a.W));
+                if (SAMP) {
+                    const uint32_t ps = pixel_seed((uint32_t)x, y, (uint32_t)a.W);
+                    rng = (pf_smp == smp && pf_pix == pix) ? (pf0 ^ pf1 ^ pf2 ^ pf3) : sample_seed(a.jt, smp, ps);
+                    // the block's next sample: its table words now, XORed at its start
+                    const uint32_t* t = a.jt + (size_t)(smp + 1u) * 1024u;
+                    const bool more = smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u;
+                    const uint32_t* tt = more ? t : a.jt;
+                    pf0 = tt[ps & 255u];
+                    pf1 = tt[256u + ((ps >> 8) & 255u)];
+                    pf2 = tt[512u + ((ps >> 16) & 255u)];
+                    pf3 = tt[768u + (ps >> 24)];
+                    pf_smp = more ? smp + 1u : 0xFFFFFFFFu;
+                    pf_pix = pix;
+                }
                 camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd);
                 start = true;
             }
