@@ -33,6 +33,7 @@ Everything else goes to stderr.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -92,6 +93,21 @@ def pmc_traffic() -> dict:
             "traffic_source": os.path.relpath(files[-1], ROOT), "traffic_kernel": rec["kernel"]}
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Point file descriptor 1 at stderr for the duration (native libraries
+    write to the descriptor, not to sys.stdout)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,10 +140,14 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if dist_on:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
-        else:
-            dist.init_process_group("gloo")
+        # RCCL prints a version banner on stdout when its communicator comes up;
+        # route it to stderr so stdout carries only rank 0's JSON line
+        with stdout_to_stderr():
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()
 
     obj, W, H, SPP, sponza = CONFIGS[args.config]
     path = scene_path(obj)

@@ -28,8 +28,10 @@ def _bench(args, env_extra=None, timeout=600):
     r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
                        env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    # the contract: stdout is exactly one JSON line (RCCL's init banner is
+    # routed to stderr by bench.py)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     return json.loads(lines[0])
 
 
