@@ -14,9 +14,12 @@ region.  value = all rays of all ranks / max-over-ranks wall time.
 Seeding (--seed-mode): "sample" (default) = every pixel's own xorshift stream
 (seed (y*W+x)*9781+1, as pixel mode) with sample s starting 2^16*s steps into
 it, so a pixel's samples are independent work units; "pixel" = one stream per
-pixel, samples in sequence (the per-pixel chain bounds strong scaling).  Both
-are byte-exact against their oracle legs (tests/); the line also reports the
-other mode's throughput (seed_modes), timed the same way after the main run.
+pixel, samples in sequence (the per-pixel chain bounds strong scaling); "row" =
+the reference's own seeding, unmodified (main.cpp:204: one stream threaded
+through a row's pixels and samples; byte-identical to the reference binary),
+run by the speculative row engine.  All three are byte-exact against their
+oracle legs (tests/); the line also reports the other modes' throughput
+(seed_modes), timed the same way after the main run.
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
   roofline      dominant kernel (k_path: all queries of the frame): algorithmic
@@ -115,7 +118,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
     ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
-    ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel"])
+    ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel", "row"])
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding mode")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the collective path (process group, gather, max-over-ranks) even at one rank "
@@ -153,7 +156,7 @@ def main() -> None:
     path = scene_path(obj)
     engine = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT,
               "mega": tm.ENGINE_MEGAKERNEL}[args.engine]
-    seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL}
+    seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL, "row": tm.SEED_ROW}
     seed = seeds[args.seed_mode]
     tris, bmin, bmax = tm.load_scene(path)
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
@@ -301,7 +304,8 @@ def main() -> None:
         osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
         t1 = time.perf_counter()
         ref, crays = osc.render(cam.as_array(), W, H, SPP,
-                                seed_mode={"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL}[args.seed_mode],
+                                seed_mode={"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL,
+                                           "row": oracle.SEED_ROW}[args.seed_mode],
                                 row_step=args.cpu_row_step, threads=threads)
         cdt = time.perf_counter() - t1
         rows = np.arange(0, H, args.cpu_row_step)

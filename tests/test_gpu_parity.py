@@ -161,18 +161,76 @@ def test_hitscene_reference_contract(gpu):
     sc.close()
 
 
+@pytest.mark.parametrize("engine", [tm.ENGINE_MEGAKERNEL, tm.ENGINE_PERSISTENT])
 @pytest.mark.parametrize("name", ["triangle", "cube", "suzanne", "teapot"])
-def test_row_mode_reproduces_reference_binary(gpu, name):
+def test_row_mode_reproduces_reference_binary(gpu, name, engine):
     """Row mode (main.cpp:204 unmodified) at 640x360x4: the GPU image is the
     reference binary's, byte for byte (SHA-256 recorded in SURVEY.md §8c), and
-    the ray count matches."""
+    the ray count matches.  Megakernel = one lane per row chain; persistent =
+    the speculative row engine (render_rowspec)."""
     tris, bmin, bmax, sc = _scene(name + ".obj")
     cam = tm.Camera.for_scene(bmin, bmax, 640, 360)
-    img, rays = sc.trace_image(cam, 640, 360, 4, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
+    img, rays = sc.trace_image(cam, 640, 360, 4, seed_mode=tm.SEED_ROW, engine=engine)
     sha, krays = REFERENCE_BINARY[name]
     assert round(rays / 1000.0, 1) == krays
     assert _png_order_sha(img) == sha
     sc.close()
+
+
+# ---------------------------------------------------------------- speculative row chains
+@pytest.mark.parametrize("wmax", [None, "8", "33"])
+@pytest.mark.parametrize("name,w,h,spp", [("suzanne.obj", 320, 180, 16), ("teapot.obj", 203, 77, 7),
+                                          ("cube.obj", 64, 1, 1), ("triangle.obj", 1, 3, 5)])
+def test_rowspec_equals_row_chains(gpu, monkeypatch, name, w, h, spp, wmax):
+    """The speculative row engine (every even RNG offset of a window traced,
+    then the chain walked through it) gives the one-lane-per-row megakernel's
+    image and ray count exactly: windows capped at 8 and 33 units force many
+    iterations per pixel and chains that leave a window mid-pixel."""
+    if wmax:
+        monkeypatch.setenv("TMPT_ROWSPEC_WMAX", wmax)
+    tris, bmin, bmax, sc = _scene(name)
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
+    b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    assert ra == rb
+    diff = np.nonzero((a != b).any(-1))
+    assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+    sc.close()
+
+
+def test_rowspec_shards_and_oracle(gpu):
+    """Row seeding over 3 interleaved shards (each row's chain is independent):
+    the tiles reassemble to the 1-shard frame, which equals the oracle's row
+    loop (main.cpp:202-233) on every 7th row."""
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    w, h, spp = 320, 180, 8
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    out = np.zeros_like(full)
+    total = 0
+    for s in range(3):
+        tile, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, band_rows=5, shard=s, num_shards=3,
+                                 engine=tm.ENGINE_PERSISTENT)
+        out[tm.tile_row_to_y(w, h, 5, s, 3)] = tile
+        total += r
+    assert np.array_equal(out, full) and total == rays
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_ROW, row_step=7)
+    rows = np.arange(0, h, 7)
+    assert np.array_equal(full[rows], ref[rows])
+    sc.close()
+
+
+def test_rowspec_bench_frame_rows(gpu, sponza_path):
+    """Bench workload (stand-in sponza 1920x1080) in row seeding at 2 spp: the
+    speculative engine equals the megakernel's row chains on the whole frame."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 2
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris) as sc:
+        a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
+        b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    assert ra == rb and np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL, tm.ENGINE_PERSISTENT])

@@ -1,0 +1,60 @@
+"""Row seeding (the reference's unmodified RNG, main.cpp:204) on the bench frame:
+the speculative row engine's variants against each other, interleaved in one
+process; every variant's image and ray count must equal the first one's.
+
+  python tools/rowspec_time.py "TMPT_ROWSPEC_GROUPS=1;TMPT_ROWSPEC_GROUPS=2&TMPT_ROWSPEC_MARGIN=1.3" [spp] [rounds]
+
+ENGINE=mega in a variant runs the one-lane-per-row megakernel instead.
+TMPT_ROWSPEC_LOG=1 prints iterations and the speculation factor per render."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "data"))
+import numpy as np  # noqa: E402
+
+import toymeshpathtracer_amd as tm  # noqa: E402
+import gen_standin_sponza  # noqa: E402
+
+KEYS = ("TMPT_ROWSPEC_GROUPS", "TMPT_ROWSPEC_MARGIN", "TMPT_ROWSPEC_WMAX", "TMPT_ROWSPEC", "TMPT_ROWSPEC_GDIV", "TMPT_ROWSPEC_CHUNK")
+
+
+def main():
+    variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
+    spp = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    W, H = map(int, os.environ.get("TUNE_RES", "1920x1080").split("x"))
+    shards = int(os.environ.get("TUNE_SHARDS", "1"))
+    tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
+    cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
+    sc = tm.Scene(tris)
+    ref = None
+    res = {v: [] for v in variants}
+    for _ in range(rounds):
+        for v in variants:
+            env = dict(kv.split("=", 1) for kv in v.split("&") if kv)
+            for k in KEYS:
+                os.environ.pop(k, None)
+            for k, val in env.items():
+                if k != "ENGINE":
+                    os.environ[k] = val
+            eng = tm.ENGINE_MEGAKERNEL if env.get("ENGINE") == "mega" else tm.ENGINE_PERSISTENT
+            t0 = time.perf_counter()
+            img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_ROW, engine=eng, band_rows=1,
+                                       shard=0, num_shards=shards)
+            dt = time.perf_counter() - t0
+            if ref is None:
+                ref = (img, rays)
+            assert rays == ref[1] and np.array_equal(img, ref[0]), f"variant {v!r} changed the image"
+            res[v].append((dt * 1e3, rays / dt / 1e6))
+            print(f"{v or 'default'}: {dt * 1e3:.1f} ms, {rays / dt / 1e6:.1f} MRays/s", flush=True)
+    for v, xs in res.items():
+        a = np.array(xs)
+        print(f"{v or 'default':>60}: frame {np.median(a[:, 0]):8.1f} ms  {np.median(a[:, 1]):7.1f} MRays/s "
+              f"({rays} rays, {spp} spp, 1/{shards} shard)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

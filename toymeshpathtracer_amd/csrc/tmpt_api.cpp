@@ -201,6 +201,13 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);
+    if (s.jt2) (void)hipFree(s.jt2);
+    if (s.rs_buf) (void)hipFree(s.rs_buf);
+    for (auto& st : s.rs_stream)
+        if (st) (void)hipStreamDestroy(st);
+    for (auto& ev : s.rs_event)
+        if (ev) (void)hipEventDestroy(ev);
+    if (s.rs_host) (void)hipHostFree(s.rs_host);
     free_shadow_grid(s);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);

@@ -102,6 +102,8 @@ constexpr float kTfarSlack = 1.00001f;
 // kStackTotal (DESIGN.md "Traversal").
 constexpr int kStackTotal = 128;
 
+constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
+
 struct Scene {
     int device = 0;
     int32_t n = 0;          // triangles incl. the floor
@@ -132,6 +134,15 @@ struct Scene {
     int32_t jt_spp = 0;
     float4* sbuf = nullptr;
     size_t sbuf_bytes = 0;
+    // speculative row seeding (tmpt_render.hip render_rowspec): jump tables
+    // M^(2j) for j in [0, jt2_n), and its row/unit buffers
+    uint32_t* jt2 = nullptr;
+    int32_t jt2_n = 0;
+    void* rs_buf = nullptr;
+    size_t rs_bytes = 0;
+    hipStream_t rs_stream[kRowSpecMaxGroups] = {};      // one per row group
+    hipEvent_t rs_event[kRowSpecMaxGroups + 1] = {};    // group ends; [max]: the start
+    uint32_t* rs_host = nullptr;                        // pinned: each group's last unit count
     int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
     hipEvent_t path_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // around the pilot / final k_path
     // statistics of the last render

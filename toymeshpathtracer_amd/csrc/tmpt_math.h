@@ -65,15 +65,23 @@ TMPT_HD float random_float01(uint32_t& state) { return key_to_float01(xorshift32
 
 // RandomInUnitDisk, maths.cpp:20-28; the draws of one argument list are taken
 // left to right (x first): SURVEY.md §0.4.
-TMPT_HD f3 random_in_unit_disk(uint32_t& state)
+// `draws` counts the RNG draws taken (2 per try; the speculative row engine
+// needs each sample's draw count, tmpt_render.hip render_rowspec).
+TMPT_HD f3 random_in_unit_disk(uint32_t& state, uint32_t& draws)
 {
     f3 p;
     do {
         float rx = random_float01(state);
         float ry = random_float01(state);
+        draws += 2u;
         p = 2.0f * mk(rx, ry, 0.0f) - mk(1.0f, 1.0f, 0.0f);
     } while (dot(p, p) >= 1.0f);
     return p;
+}
+TMPT_HD f3 random_in_unit_disk(uint32_t& state)
+{
+    uint32_t draws = 0;
+    return random_in_unit_disk(state, draws);
 }
 
 // Angle of RandomUnitVector for a 24-bit key, maths.cpp:34: (r * 2) * kPI.
@@ -175,21 +183,35 @@ struct Camera {
 };
 
 // Camera::GetRay, maths.h:93-104
-TMPT_HD void camera_get_ray(const Camera& c, float s, float t, uint32_t& state, f3& o, f3& d)
+TMPT_HD void camera_get_ray(const Camera& c, float s, float t, uint32_t& state, f3& o, f3& d,
+                            uint32_t& draws)
 {
-    f3 rd = c.lens_radius * random_in_unit_disk(state);
+    f3 rd = c.lens_radius * random_in_unit_disk(state, draws);
     f3 offset = c.u * rd.x + c.v * rd.y;
     o = c.origin + offset;
     d = normalize(c.lower_left + s * c.horizontal + t * c.vertical - c.origin - offset);
 }
+TMPT_HD void camera_get_ray(const Camera& c, float s, float t, uint32_t& state, f3& o, f3& d)
+{
+    uint32_t draws = 0;
+    camera_get_ray(c, s, t, state, o, d, draws);
+}
 
-// One camera sample of TraceImageBody, main.cpp:212-216 (draws left to right).
+// One camera sample of TraceImageBody, main.cpp:212-216 (draws left to right);
+// `draws` += the RNG draws it took (2 + 2 per disk try).
 TMPT_HD void camera_sample(const Camera& c, uint32_t x, uint32_t y, float invW, float invH,
-                           uint32_t& state, f3& o, f3& d)
+                           uint32_t& state, f3& o, f3& d, uint32_t& draws)
 {
     float su = ((float)x + random_float01(state)) * invW;
     float sv = ((float)y + random_float01(state)) * invH;
-    camera_get_ray(c, su, sv, state, o, d);
+    draws += 2u;
+    camera_get_ray(c, su, sv, state, o, d, draws);
+}
+TMPT_HD void camera_sample(const Camera& c, uint32_t x, uint32_t y, float invW, float invH,
+                           uint32_t& state, f3& o, f3& d)
+{
+    uint32_t draws = 0;
+    camera_sample(c, x, y, invW, invH, state, o, d, draws);
 }
 
 // ---------------------------------------------------------------- geometry

@@ -632,6 +632,15 @@ struct PathCtl {
     float4* __restrict__ sbuf;
     uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp
     int sb_nt;              // nontemporal stores
+    // Speculative row seeding (SAMP 2, render_rowspec): unit u traces ONE
+    // sample of tile pixel upix[u] from RNG state ustate[u] and writes its
+    // colour with w = draws | rays << 27 to rs_out[u], and its final RNG state
+    // to rs_end[u]
+    const uint32_t* __restrict__ upix;
+    const uint32_t* __restrict__ ustate;
+    float4* __restrict__ rs_out;
+    uint32_t* __restrict__ rs_end;
+    const uint32_t* __restrict__ p_dev;  // the unit count (replaces P, nchunks at launch)
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -710,6 +719,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
     uint32_t res = 0, res_end = 0;
+    if (SAMP == 2) {  // the speculative row engine plans its units on the device
+        pc.P = *pc.p_dev;
+        pc.nchunks = (uint32_t)((pc.P + pc.chunk - 1) / pc.chunk);
+    }
     bool exhausted = pc.P == 0;
     if (kFull && pc.simd_reg && !exhausted) {  // SIMD-balanced first chunk
         const uint2 rd = simd_rank(pc.simd_reg);
@@ -748,6 +761,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     // camera phase ahead (pf_smp = the sample they belong to), so a new sample
     // does not wait for their memory round trip
     uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf_smp = 0xFFFFFFFFu, pf_pix = 0;
+    // SAMP 2: the unit held, the ray counts at its start, the camera's RNG draws
+    uint32_t cur_unit = 0, re0 = 0, rs0 = 0, ndraw = 0;
     uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
     uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
     uint32_t pt0 = 0, pnsh = 0;  // PROF + tlog: pixel start time, shading rounds while held
@@ -826,7 +841,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
                     uint32_t smp0 = (uint32_t)a.smp_begin;
-                    if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
+                    if (SAMP == 2) {  // speculative row seeding: one sample from a given state
+                        cur_unit = res + k;
+                        pix = pc.upix[cur_unit];
+                        re0 = rays_e;
+                        rs0 = rays_s;
+                    } else if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
                         const uint32_t unit = res + k;
                         pix = unit / pc.nblk;
                         smp0 = (unit - pix * pc.nblk) * pc.blk;
@@ -842,7 +862,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                    if (!kFull || a.smp_begin == 0) {
+                    if (SAMP == 2) {
+                        rng = pc.ustate[cur_unit];
+                    } else if (!kFull || a.smp_begin == 0) {
                         rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
                         col = mk(0.0f, 0.0f, 0.0f);
                     } else {  // progressive: continue the previous pass's stream and sum
@@ -984,7 +1006,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (!pend) {
                     for (int kk = (int)depth - 1; kk >= 0; --kk)
                         color = backward_step(color, light[kk * BLOCK]);
-                    if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve sums in sample order
+                    if (SAMP == 2) {  // speculative row seeding: render_rowspec's chase consumes it
+                        // draws: the camera's, and RandomUnitVector's 2 at each of the
+                        // `depth` hits (main.cpp:71, drawn at the 10th hit too)
+                        const uint32_t draws = ndraw + 2u * depth;
+                        const uint32_t ne = rays_e - re0, nr = ne + rays_s - rs0;  // <= 10, <= 20
+                        pc.rs_out[cur_unit] =
+                            make_float4(color.x, color.y, color.z, __uint_as_float(draws | (nr << 23) | (ne << 28)));
+                        pc.rs_end[cur_unit] = rng;
+                    } else if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve sums in sample order
                         float4* dst = pc.sbuf + ((size_t)smp * pc.sb_ss + (size_t)pix * pc.sb_sp);
                         const float4 v = make_float4(color.x, color.y, color.z, 0.0f);
                         if (pc.sb_nt) {
@@ -1012,7 +1042,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             pc.tlog[4 * (size_t)pix + 3] = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) |
                                                            (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu);
                         }
-                        if (!SAMP || !pc.sbuf)
+                        if (SAMP != 2 && (!SAMP || !pc.sbuf))
                             out[pix] = (COUNT && pc.cost_map)
                                            ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
                                                                : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
@@ -1031,7 +1061,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const int lr = (int)(pix / (uint32_t)a.W);
                 const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
                 const uint32_t y = (uint32_t)tile_row_to_y(a, lr);
-                if (SAMP) {
+                if (SAMP == 1) {
                     const uint32_t ps = pixel_seed((uint32_t)x, y, (uint32_t)a.W);
                     rng = (pf_smp == smp && pf_pix == pix) ? (pf0 ^ pf1 ^ pf2 ^ pf3) : sample_seed(a.jt, smp, ps);
                     // the block's next sample: its table words now, XORed at its start
@@ -1045,7 +1075,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     pf_smp = more ? smp + 1u : 0xFFFFFFFFu;
                     pf_pix = pix;
                 }
-                camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd);
+                if (SAMP == 2) {
+                    ndraw = 0;
+                    camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd, ndraw);
+                } else {
+                    camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd);
+                }
                 start = true;
             }
             if (PROF >= 2) {
@@ -1261,6 +1296,163 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
     if (t < np) out[p0 + t] = pack_pixel(col, spp_recip);
 }
 
+// ============================================================ speculative row seeding
+// Row seeding (main.cpp:204) threads ONE xorshift stream through a row's
+// pixels and samples, and a sample's draws depend on its path, so a row is a
+// sequential chain (the megakernel runs one lane per row).  But a sample is
+// a pure function of (pixel, start state), and every draw site takes two
+// draws (maths.cpp:25, 32-33, main.cpp:214-215), so the next sample starts
+// an even number of draws after this one's start.  render_rowspec traces,
+// for each row, one sample at EVERY even offset 2j of a window past the
+// row's current state (units of k_path<SAMP 2>), then a chase walks the
+// chain through the window: take the sample at offset 0, add its colour in
+// sample order, jump to offset + its draws, ...  Each window costs ~draws/2
+// traces per chain sample (speculation), but all of them run in parallel.
+struct RowSpec {
+    int row0, nrows;  // this group's tile rows [row0, row0 + nrows)
+    // per row of the group: chain state, current pixel and samples done in it,
+    // its draws so far and the previous pixel's mean draws per sample (window
+    // sizing), chain rays (all, closest-hit), window, unit offsets (nrows + 1)
+    uint32_t *rng, *x, *k, *pdraws, *prev_mean, *rays, *erays, *win, *offs;
+    uint32_t* short_win;  // iterations whose window ended before the pixel did (diagnostic)
+    float4* col;
+    uint32_t* total;  // units of this iteration
+    uint32_t wmax;
+    float margin;
+};
+
+// Decode of a unit's rs_out.w: draws | rays << 23 | extend rays << 28.
+constexpr uint32_t kRsDrawBits = 23;
+
+__global__ void __launch_bounds__(256) k_rs_init(RenderArgs a, RowSpec rs)
+{
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= rs.nrows) return;
+    rs.rng[r] = row_seed((uint32_t)tile_row_to_y(a, rs.row0 + r));  // main.cpp:204, unmodified
+    rs.x[r] = rs.k[r] = rs.pdraws[r] = rs.rays[r] = rs.erays[r] = rs.short_win[r] = 0u;
+    rs.prev_mean[r] = __float_as_uint(17.0f);  // draws per sample before any is seen
+    rs.col[r] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// Window per row: the remaining samples of its pixel at the larger of this
+// pixel's and the previous pixel's mean draws per sample, x margin, over 2
+// (even offsets only); exclusive scan into offs; total units.  One block.
+__global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
+{
+    __shared__ uint32_t part[1024];
+    const int rows = rs.nrows;
+    const int per = (rows + 1023) / 1024;
+    const int r0 = min(rows, (int)threadIdx.x * per), r1 = min(rows, r0 + per);
+    uint32_t sum = 0;
+    for (int r = r0; r < r1; ++r) {
+        uint32_t w = 0;
+        if (rs.x[r] < (uint32_t)a.W) {
+            const uint32_t k = rs.k[r];
+            float mean = __uint_as_float(rs.prev_mean[r]);
+            if (k > 0) mean = fmaxf(mean, (float)rs.pdraws[r] / (float)k);
+            const float rem = (float)((uint32_t)a.spp - k);
+            w = min(rs.wmax, (uint32_t)(rem * mean * 0.5f * rs.margin) + 2u);
+        }
+        rs.win[r] = w;
+        sum += w;
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the thread sums
+        const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t o = part[threadIdx.x] - sum;
+    for (int r = r0; r < r1; ++r) {
+        rs.offs[r] = o;
+        o += rs.win[r];
+    }
+    if (threadIdx.x == 1023) {
+        rs.offs[rows] = part[1023];
+        *rs.total = part[1023];
+    }
+}
+
+// Unit u -> (row, offset index j): pixel and start state M^(2j) rng[row].
+// Launched over the largest possible count; the plan's total bounds it.
+__global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const uint32_t* __restrict__ jt2,
+                                                 uint32_t* __restrict__ upix, uint32_t* __restrict__ ustate)
+{
+    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= *rs.total) return;
+    int lo = 0, hi = rs.nrows - 1;  // last row with offs <= u
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rs.offs[mid] <= u) lo = mid;
+        else hi = mid - 1;
+    }
+    const uint32_t j = u - rs.offs[lo];
+    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo];
+    ustate[u] = sample_seed(jt2, j, rs.rng[lo]);
+}
+
+// The chase, one thread per row: the chain's samples in order through the
+// window (main.cpp:209-219), the pixel packed after its spp-th (:221-233).
+__global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const float4* __restrict__ rs_out,
+                                                 const uint32_t* __restrict__ rs_end, uint32_t* __restrict__ out)
+{
+    const int r = blockIdx.x * 64 + threadIdx.x;
+    if (r >= rs.nrows) return;
+    const uint32_t n = rs.win[r];
+    if (n == 0) return;
+    const uint32_t base = rs.offs[r];
+    uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
+    const float4 c0 = rs.col[r];
+    f3 col = mk(c0.x, c0.y, c0.z);
+    uint32_t j = 0, last = 0xFFFFFFFFu;
+    while (j < n) {
+        const float4 t = rs_out[base + j];
+        const uint32_t w = __float_as_uint(t.w);
+        const uint32_t draws = w & ((1u << kRsDrawBits) - 1u);
+        rays += (w >> kRsDrawBits) & 31u;
+        erays += w >> 28;
+        pdraws += draws;
+        col = col + mk(t.x, t.y, t.z);  // col += Trace(...), main.cpp:218
+        last = j;
+        j += draws >> 1;
+        if (++k == (uint32_t)a.spp) {  // the rest of the window belongs to this pixel: dropped
+            out[(size_t)(rs.row0 + r) * a.W + x] = pack_pixel(col, a.spp_recip);
+            rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
+            ++x;
+            k = 0;
+            pdraws = 0;
+            col = mk(0.0f, 0.0f, 0.0f);
+            break;
+        }
+    }
+    if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[base + last];  // the next sample's start state
+    if (k != 0) ++rs.short_win[r];
+    rs.k[r] = k;
+    rs.x[r] = x;
+    rs.pdraws[r] = pdraws;
+    rs.rays[r] = rays;
+    rs.erays[r] = erays;
+    rs.col[r] = make_float4(col.x, col.y, col.z, 0.0f);
+}
+
+// The chain's rays (the reference's count): counters[0] all, [3] closest-hit.
+__global__ void __launch_bounds__(256) k_rs_count(RowSpec rs, unsigned long long* counters)
+{
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t v = r < rs.nrows ? rs.rays[r] : 0u, e = r < rs.nrows ? rs.erays[r] : 0u;
+    unsigned long long sv = v, se = e;
+    for (int off = 32; off > 0; off >>= 1) {
+        sv += __shfl_xor(sv, off);
+        se += __shfl_xor(se, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&counters[0], sv);
+        atomicAdd(&counters[3], se);
+    }
+}
+
 // ============================================================ host side
 namespace {
 
@@ -1329,21 +1521,24 @@ void xorshift_power(uint64_t n, uint32_t* acc)
 
 }  // namespace
 
-// sample_seed's byte tables for samples [0, spp): J_s = M^(s * kSampleStride)
-void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab)
+// sample_seed's byte tables for jumps J_i = M^(i * stride), i in [0, count)
+void jump_tables(uint64_t stride_steps, int32_t count, std::vector<uint32_t>& tab)
 {
     uint32_t stride[32], J[32];
-    xorshift_power(kSampleStride, stride);
+    xorshift_power(stride_steps, stride);
     for (int j = 0; j < 32; ++j) J[j] = 1u << j;
-    tab.assign((size_t)spp * 1024u, 0u);
-    for (int32_t smp = 0; smp < spp; ++smp) {
-        uint32_t* t = tab.data() + (size_t)smp * 1024u;
+    tab.assign((size_t)count * 1024u, 0u);
+    for (int32_t i = 0; i < count; ++i) {
+        uint32_t* t = tab.data() + (size_t)i * 1024u;
         for (int k = 0; k < 4; ++k)
             for (uint32_t b = 1; b < 256; ++b)  // table[b] = table[b without its lowest bit] ^ column
                 t[256 * k + b] = t[256 * k + (b & (b - 1u))] ^ J[8 * k + __builtin_ctz(b)];
         gf2_mul(stride, J, J);
     }
 }
+
+// sample_seed's byte tables for samples [0, spp): J_s = M^(s * kSampleStride)
+void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab) { jump_tables(kSampleStride, spp, tab); }
 
 namespace {
 
@@ -1950,6 +2145,201 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     return 0;
 }
 
+// Speculative row seeding (k_rs_* above): iterations of plan -> fill ->
+// k_path<SAMP 2> -> chase until every row of the tile has its W pixels.  Each
+// iteration moves every unfinished row through (usually) one pixel.  The rows
+// are split into G groups, each iterating on its own stream, so one group's
+// k_path tail overlaps another's work; the unit counts stay on the device and
+// the host only checks for completion every kCheck iterations.
+int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
+{
+    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2, kCheck = 64;
+    auto fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 2>;
+    const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const int rows = a.tile_rows;
+    // window cap: one iteration covers a pixel's samples at up to 2 * wmax / spp
+    // = 48 draws per sample (the stand-in sponza averages ~17, its deepest rows
+    // ~25; a cap of 24 draws left those rows one short window per pixel, and
+    // the slowest row sets the iteration count)
+    uint32_t wmax = (uint32_t)std::min<int64_t>(8192, std::max<int64_t>(64, (int64_t)a.spp * 24));
+    if (const char* e = getenv("TMPT_ROWSPEC_WMAX")) wmax = (uint32_t)std::max(8, std::min(16384, atoi(e)));
+    float margin = 1.15f;  // window = expected draws x margin
+    if (const char* e = getenv("TMPT_ROWSPEC_MARGIN")) margin = std::max(0.1f, (float)atof(e));
+    int G = 2;  // row groups (streams)
+    if (const char* e = getenv("TMPT_ROWSPEC_GROUPS")) G = atoi(e);
+    G = std::max(1, std::min(std::min(G, kRowSpecMaxGroups), rows));
+    // each group's k_path gets grid / gdiv blocks: with gdiv = G the groups'
+    // kernels share the GPU at once instead of queueing behind each other
+    int gdiv = 1;
+    if (const char* e = getenv("TMPT_ROWSPEC_GDIV")) gdiv = std::max(1, std::min(16, atoi(e)));
+    const int pgrid = std::max(1, grid / gdiv);
+    // units a wave reserves at once (a launch holds ~1.5 units per lane, so
+    // smaller reservations balance the waves' loads)
+    uint32_t chunk = kChunk;
+    if (const char* e = getenv("TMPT_ROWSPEC_CHUNK")) chunk = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (s.jt2_n < (int32_t)wmax) {  // J_j = M^(2j): the state 2j draws on
+        std::vector<uint32_t> tab;
+        jump_tables(2, (int32_t)wmax, tab);
+        uint32_t* nt = nullptr;
+        TMPT_HIP(hipMalloc(&nt, tab.size() * sizeof(uint32_t)));
+        if (hipMemcpy(nt, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(nt);
+            set_error("tmpt_render: jump table upload failed");
+            return -1;
+        }
+        if (s.jt2) (void)hipFree(s.jt2);
+        s.jt2 = nt;
+        s.jt2_n = (int32_t)wmax;
+    }
+    const size_t ovf_words = (size_t)pgrid * kBlk * (kStackTotal - kPathSL);
+    const size_t head_words = (size_t)kSeg * kCtr;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    auto group_rows = [&](int g) { return rows / G + (g < rows % G ? 1 : 0); };
+    auto group_bytes = [&](int g) {
+        const size_t R = (size_t)group_rows(g), U = R * wmax;
+        return al(U * (sizeof(float4) + 3 * sizeof(uint32_t)) + R * sizeof(float4) + (10 * R + 2) * sizeof(uint32_t) +
+                  (ovf_words + head_words) * sizeof(uint32_t));
+    };
+    size_t need = al(24 * sizeof(unsigned long long));
+    for (int g = 0; g < G; ++g) need += group_bytes(g);
+    if (s.rs_bytes < need) {
+        if (s.rs_buf) (void)hipFree(s.rs_buf);
+        s.rs_buf = nullptr;
+        s.rs_bytes = 0;
+        TMPT_HIP(hipMalloc(&s.rs_buf, need));
+        s.rs_bytes = need;
+    }
+    if (!s.rs_host) TMPT_HIP(hipHostMalloc((void**)&s.rs_host, kRowSpecMaxGroups * sizeof(uint32_t)));
+    for (int g = 0; g < G; ++g)
+        if (!s.rs_stream[g]) {
+            TMPT_HIP(hipStreamCreateWithFlags(&s.rs_stream[g], hipStreamNonBlocking));
+            TMPT_HIP(hipEventCreateWithFlags(&s.rs_event[g], hipEventDisableTiming));
+        }
+    if (!s.rs_event[kRowSpecMaxGroups]) TMPT_HIP(hipEventCreateWithFlags(&s.rs_event[kRowSpecMaxGroups], hipEventDisableTiming));
+    char* p = static_cast<char*>(s.rs_buf);
+    unsigned long long* spec_ctr = reinterpret_cast<unsigned long long*>(p);  // every traced unit's rays
+    p += al(24 * sizeof(unsigned long long));
+    struct Group {
+        RowSpec rs;
+        PathCtl pc;
+        float4* rs_out;
+        uint32_t *upix, *ustate, *rs_end, *heads, *ovf;
+        size_t U;
+        hipStream_t st;
+    };
+    std::vector<Group> gs(G);
+    RenderArgs as = a;
+    as.jt = nullptr;
+    as.bmask = 0u;  // every unit is one sample
+    as.smp_begin = 0;
+    as.smp_end = a.spp;
+    int row0 = 0;
+    for (int g = 0; g < G; ++g) {
+        Group& q = gs[g];
+        char* gp = p;
+        p += group_bytes(g);
+        const size_t R = (size_t)group_rows(g);
+        q.U = R * wmax;
+        q.st = s.rs_stream[g];
+        q.rs.row0 = row0;
+        q.rs.nrows = (int)R;
+        q.rs.wmax = wmax;
+        q.rs.margin = margin;
+        row0 += (int)R;
+        q.rs_out = reinterpret_cast<float4*>(gp);
+        gp += q.U * sizeof(float4);
+        q.rs.col = reinterpret_cast<float4*>(gp);
+        gp += R * sizeof(float4);
+        uint32_t* w = reinterpret_cast<uint32_t*>(gp);
+        q.upix = w;
+        q.ustate = q.upix + q.U;
+        q.rs_end = q.ustate + q.U;
+        w = q.rs_end + q.U;
+        uint32_t** fields[] = {&q.rs.rng, &q.rs.x, &q.rs.k, &q.rs.pdraws, &q.rs.prev_mean,
+                               &q.rs.rays, &q.rs.erays, &q.rs.win, &q.rs.short_win};
+        for (uint32_t** f : fields) {
+            *f = w;
+            w += R;
+        }
+        q.rs.offs = w;  // rows + 1
+        w += R + 1;
+        q.rs.total = w;
+        w += 1;
+        q.ovf = w;
+        q.heads = w + ovf_words;
+        memset(&q.pc, 0, sizeof(q.pc));
+        q.pc.heads = q.heads;
+        q.pc.nblk = q.pc.blk = 1u;
+        q.pc.lane_cap = 64u;
+        q.pc.chunk = chunk;
+        q.pc.upix = q.upix;
+        q.pc.ustate = q.ustate;
+        q.pc.rs_out = q.rs_out;
+        q.pc.rs_end = q.rs_end;
+        q.pc.p_dev = q.rs.total;
+    }
+    // the groups start after the work already on the scene's stream (the
+    // caller's wait), and that stream resumes after all of them
+    TMPT_HIP(hipMemsetAsync(spec_ctr, 0, 24 * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipEventRecord(s.rs_event[kRowSpecMaxGroups], s.stream));
+    for (Group& q : gs) {
+        TMPT_HIP(hipStreamWaitEvent(q.st, s.rs_event[kRowSpecMaxGroups], 0));
+        k_rs_init<<<(unsigned)((q.rs.nrows + 255) / 256), 256, 0, q.st>>>(a, q.rs);
+    }
+    TMPT_HIP(hipGetLastError());
+    int it = 0;
+    // every iteration moves each unfinished row by >= 1 sample, so W * spp bounds them
+    const int64_t max_it = (int64_t)a.W * a.spp + kCheck;
+    for (bool done = false; !done && it < max_it;) {
+        for (int c = 0; c < kCheck; ++c, ++it)
+            for (Group& q : gs) {
+                k_rs_plan<<<1, 1024, 0, q.st>>>(a, q.rs);
+                k_rs_fill<<<(unsigned)((q.U + 255) / 256), 256, 0, q.st>>>(a, q.rs, s.jt2, q.upix, q.ustate);
+                TMPT_HIP(hipMemsetAsync(q.heads, 0, head_words * 4, q.st));
+                fn<<<pgrid, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
+                k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, d_out);
+            }
+        TMPT_HIP(hipGetLastError());
+        // the last plan of each group: 0 units = the group was already done
+        for (int g = 0; g < G; ++g)
+            TMPT_HIP(hipMemcpyAsync(&s.rs_host[g], gs[g].rs.total, 4, hipMemcpyDeviceToHost, gs[g].st));
+        done = true;
+        for (int g = 0; g < G; ++g) {
+            TMPT_HIP(hipStreamSynchronize(gs[g].st));
+            done = done && s.rs_host[g] == 0;
+        }
+    }
+    for (int g = 0; g < G; ++g) {
+        k_rs_count<<<(unsigned)((gs[g].rs.nrows + 255) / 256), 256, 0, gs[g].st>>>(gs[g].rs, d_counters);
+        TMPT_HIP(hipEventRecord(s.rs_event[g], gs[g].st));
+        TMPT_HIP(hipStreamWaitEvent(s.stream, s.rs_event[g], 0));
+    }
+    TMPT_HIP(hipGetLastError());
+    s.path_launches = it;
+    if (getenv("TMPT_ROWSPEC_LOG")) {
+        unsigned long long c[2] = {0, 0};
+        TMPT_HIP(hipMemcpyAsync(c, d_counters, sizeof(c), hipMemcpyDeviceToHost, s.stream));
+        unsigned long long t = 0;
+        TMPT_HIP(hipMemcpyAsync(&t, spec_ctr, sizeof(t), hipMemcpyDeviceToHost, s.stream));
+        std::vector<uint32_t> sw(rows);
+        for (Group& q : gs)
+            TMPT_HIP(hipMemcpyAsync(sw.data() + q.rs.row0, q.rs.short_win, q.rs.nrows * 4, hipMemcpyDeviceToHost, s.stream));
+        TMPT_HIP(hipStreamSynchronize(s.stream));
+        uint64_t swsum = 0;
+        uint32_t swmax = 0;
+        for (uint32_t v : sw) {
+            swsum += v;
+            swmax = std::max(swmax, v);
+        }
+        fprintf(stderr,
+                "rowspec: %d iterations enqueued, %d groups of %d blocks, window cap %u, margin %.2f, traced rays "
+                "%llu for %llu chain rays (x%.2f); short windows per row: mean %.1f max %u\n",
+                it, G, pgrid, wmax, margin, t, c[0], c[0] ? (double)t / (double)c[0] : 0.0,
+                rows ? (double)swsum / rows : 0.0, swmax);
+    }
+    return 0;
+}
+
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
                     float* d_hits, int32_t* d_ids)
 {
@@ -2045,6 +2435,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     int rc = 0;
     bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode != TMPT_SEED_ROW;
     bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode != TMPT_SEED_ROW && use_wide();
+    // row seeding on the persistent engine: the speculative row chains
+    // (render_rowspec); instrumented renders and TMPT_ROWSPEC=0 run the
+    // megakernel's one lane per row
+    const char* rse = getenv("TMPT_ROWSPEC");
+    const bool rowspec = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_ROW && use_wide() &&
+                         !count && !progressive && !(rse && atoi(rse) == 0);
     if (progressive && !persistent) {
         set_error("tmpt_render: progressive spp needs the persistent engine (TMPT_BVH=2 is BVH2-only)");
         (void)hipEventDestroy(e0);
@@ -2059,6 +2455,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
+        else if (rowspec) rc = render_rowspec(s, a, d_out, d_counters);
         else rc = render_megakernel(s, a, d_out, count, d_counters);
     }
     (void)hipEventRecord(e1, s.stream);
@@ -2117,6 +2514,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
                     "(%.1f wanting, %.1f traversing)\n",
                     c[6], c[6] ? (double)c[7] / c[6] : 0.0, c[8], c[8] ? (double)c[9] / c[8] : 0.0,
                     c[10], c[10] ? (double)c[11] / c[10] : 0.0, c[10] ? (double)c[12] / c[10] : 0.0);
+    } else if (rowspec) {
+        s.extend_ms = ms;
+        s.extend_rays = c[3];
+        s.shadow_rays = c[0] - c[3];
+        s.extend_launches = s.path_launches;
+        s.iterations = s.path_launches;
     } else if (!wave) {
         s.extend_ms = ms;
         s.extend_rays = c[0];
