@@ -1317,6 +1317,7 @@ struct RowSpec {
     uint32_t* short_win;  // iterations whose window ended before the pixel did (diagnostic)
     float4* col;
     uint32_t* total;  // units of this iteration
+    unsigned long long* planned;  // units over all iterations (diagnostic)
     uint32_t wmax;
     float margin;
 };
@@ -1372,6 +1373,7 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     if (threadIdx.x == 1023) {
         rs.offs[rows] = part[1023];
         *rs.total = part[1023];
+        atomicAdd(rs.planned, (unsigned long long)part[1023]);
     }
 }
 
@@ -2277,6 +2279,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.pc.rs_out = q.rs_out;
         q.pc.rs_end = q.rs_end;
         q.pc.p_dev = q.rs.total;
+        q.rs.planned = spec_ctr + 8;
     }
     // the groups start after the work already on the scene's stream (the
     // caller's wait), and that stream resumes after all of them
@@ -2321,10 +2324,22 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         TMPT_HIP(hipMemcpyAsync(c, d_counters, sizeof(c), hipMemcpyDeviceToHost, s.stream));
         unsigned long long t = 0;
         TMPT_HIP(hipMemcpyAsync(&t, spec_ctr, sizeof(t), hipMemcpyDeviceToHost, s.stream));
-        std::vector<uint32_t> sw(rows);
-        for (Group& q : gs)
+        std::vector<uint32_t> sw(rows), pm(rows);
+        for (Group& q : gs) {
             TMPT_HIP(hipMemcpyAsync(sw.data() + q.rs.row0, q.rs.short_win, q.rs.nrows * 4, hipMemcpyDeviceToHost, s.stream));
+            TMPT_HIP(hipMemcpyAsync(pm.data() + q.rs.row0, q.rs.prev_mean, q.rs.nrows * 4, hipMemcpyDeviceToHost, s.stream));
+        }
         TMPT_HIP(hipStreamSynchronize(s.stream));
+        double pmsum = 0.0;
+        for (uint32_t v : pm) {
+            float f;
+            memcpy(&f, &v, 4);
+            pmsum += f;
+        }
+        unsigned long long planned = 0;
+        TMPT_HIP(hipMemcpy(&planned, spec_ctr + 8, sizeof(planned), hipMemcpyDeviceToHost));
+        fprintf(stderr, "rowspec: last pixel's draws per sample, mean over rows %.2f; units planned %llu (%.1f rays each)\n",
+                rows ? pmsum / rows : 0.0, planned, planned ? (double)t / (double)planned : 0.0);
         uint64_t swsum = 0;
         uint32_t swmax = 0;
         for (uint32_t v : sw) {
