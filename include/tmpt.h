@@ -49,7 +49,9 @@ enum {
     TMPT_ENGINE_WAVEFRONT = 0,  /* generate/extend/shade/shadow kernels over compacted queues */
     TMPT_ENGINE_MEGAKERNEL = 1, /* one lane per pixel (pixel mode) or per row (row mode) */
     TMPT_ENGINE_PERSISTENT = 2  /* pixel mode: one persistent kernel per frame, lanes own pixels and
-                                   schedule extend / shadow / shade per wave (row mode: megakernel) */
+                                   schedule extend / shadow / shade per wave (row mode: the speculative
+                                   row engine -- every even RNG offset of a window traced, the chain
+                                   walked through it; instrumented row renders: megakernel) */
 };
 
 /* render flags */
