@@ -178,16 +178,20 @@ def test_row_mode_reproduces_reference_binary(gpu, name, engine):
 
 
 # ---------------------------------------------------------------- speculative row chains
-@pytest.mark.parametrize("wmax", [None, "8", "33"])
+@pytest.mark.parametrize("env", [{}, {"TMPT_ROWSPEC_WMAX": "8"}, {"TMPT_ROWSPEC_WMAX": "33"},
+                                 {"TMPT_ROWSPEC_LOOK": "0"}, {"TMPT_ROWSPEC_LOOK": "0", "TMPT_ROWSPEC_WMAX": "33"},
+                                 {"TMPT_ROWSPEC_LO": "0.3", "TMPT_ROWSPEC_MARGIN": "0.6"}])
 @pytest.mark.parametrize("name,w,h,spp", [("suzanne.obj", 320, 180, 16), ("teapot.obj", 203, 77, 7),
                                           ("cube.obj", 64, 1, 1), ("triangle.obj", 1, 3, 5)])
-def test_rowspec_equals_row_chains(gpu, monkeypatch, name, w, h, spp, wmax):
+def test_rowspec_equals_row_chains(gpu, monkeypatch, name, w, h, spp, env):
     """The speculative row engine (every even RNG offset of a window traced,
-    then the chain walked through it) gives the one-lane-per-row megakernel's
-    image and ray count exactly: windows capped at 8 and 33 units force many
-    iterations per pixel and chains that leave a window mid-pixel."""
-    if wmax:
-        monkeypatch.setenv("TMPT_ROWSPEC_WMAX", wmax)
+    then the chain walked through it, into the next pixel's lookahead window
+    when its first sample falls there) gives the one-lane-per-row megakernel's
+    image and ray count exactly: windows capped at 8 and 33 units, or sized
+    short, force many iterations per pixel, chains that leave a window
+    mid-pixel and next pixels that start before or after the lookahead."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     tris, bmin, bmax, sc = _scene(name)
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)

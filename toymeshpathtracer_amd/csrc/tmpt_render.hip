@@ -1314,12 +1314,16 @@ struct RowSpec {
     // its draws so far and the previous pixel's mean draws per sample (window
     // sizing), chain rays (all, closest-hit), window, unit offsets (nrows + 1)
     uint32_t *rng, *x, *k, *pdraws, *prev_mean, *rays, *erays, *win, *offs;
+    // lookahead window of the next pixel: offsets [s2, s2 + win2) (win2 = 0: none)
+    uint32_t *win2, *s2;
     uint32_t* short_win;  // iterations whose window ended before the pixel did (diagnostic)
     float4* col;
     uint32_t* total;  // units of this iteration
     unsigned long long* planned;  // units over all iterations (diagnostic)
     uint32_t wmax;
     float margin;
+    float look_lo;  // lookahead window start, as a fraction of the current pixel's expected draws
+    int look;       // lookahead on
 };
 
 // Decode of a unit's rs_out.w: draws | rays << 23 | extend rays << 28.
@@ -1346,16 +1350,24 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     const int r0 = min(rows, (int)threadIdx.x * per), r1 = min(rows, r0 + per);
     uint32_t sum = 0;
     for (int r = r0; r < r1; ++r) {
-        uint32_t w = 0;
+        uint32_t w = 0, w2 = 0, s2 = 0;
         if (rs.x[r] < (uint32_t)a.W) {
             const uint32_t k = rs.k[r];
             float mean = __uint_as_float(rs.prev_mean[r]);
             if (k > 0) mean = fmaxf(mean, (float)rs.pdraws[r] / (float)k);
             const float rem = (float)((uint32_t)a.spp - k);
             w = min(rs.wmax, (uint32_t)(rem * mean * 0.5f * rs.margin) + 2u);
+            // lookahead: the next pixel from look_lo of this one's expected end
+            // through one pixel's window past this window's end
+            if (rs.look && rs.x[r] + 1u < (uint32_t)a.W) {
+                s2 = min(w, (uint32_t)(rem * mean * 0.5f * rs.look_lo));
+                w2 = min(rs.wmax, (w - s2) + (uint32_t)((float)a.spp * mean * 0.5f * rs.margin) + 2u);
+            }
         }
         rs.win[r] = w;
-        sum += w;
+        rs.win2[r] = w2;
+        rs.s2[r] = s2;
+        sum += w + w2;
     }
     part[threadIdx.x] = sum;
     __syncthreads();
@@ -1368,7 +1380,7 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     uint32_t o = part[threadIdx.x] - sum;
     for (int r = r0; r < r1; ++r) {
         rs.offs[r] = o;
-        o += rs.win[r];
+        o += rs.win[r] + rs.win2[r];
     }
     if (threadIdx.x == 1023) {
         rs.offs[rows] = part[1023];
@@ -1390,8 +1402,10 @@ __global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const
         if (rs.offs[mid] <= u) lo = mid;
         else hi = mid - 1;
     }
-    const uint32_t j = u - rs.offs[lo];
-    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo];
+    const uint32_t l = u - rs.offs[lo], w = rs.win[lo];
+    const bool ahead = l >= w;  // the lookahead window: the next pixel
+    const uint32_t j = ahead ? rs.s2[lo] + (l - w) : l;
+    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo] + (ahead ? 1u : 0u);
     ustate[u] = sample_seed(jt2, j, rs.rng[lo]);
 }
 
@@ -1404,32 +1418,39 @@ __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const
     if (r >= rs.nrows) return;
     const uint32_t n = rs.win[r];
     if (n == 0) return;
-    const uint32_t base = rs.offs[r];
+    const uint32_t base = rs.offs[r], n2 = rs.win2[r], s2 = rs.s2[r];
     uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
     const float4 c0 = rs.col[r];
     f3 col = mk(c0.x, c0.y, c0.z);
-    uint32_t j = 0, last = 0xFFFFFFFFu;
-    while (j < n) {
-        const float4 t = rs_out[base + j];
+    // window 0: this pixel, offsets [0, n) at base; window 1: the next pixel,
+    // offsets [s2, s2 + n2) at base + n
+    uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, hi = n, wb = base;
+    while (j >= lo && j < hi) {
+        const uint32_t idx = wb + (j - lo);
+        const float4 t = rs_out[idx];
         const uint32_t w = __float_as_uint(t.w);
         const uint32_t draws = w & ((1u << kRsDrawBits) - 1u);
         rays += (w >> kRsDrawBits) & 31u;
         erays += w >> 28;
         pdraws += draws;
         col = col + mk(t.x, t.y, t.z);  // col += Trace(...), main.cpp:218
-        last = j;
+        last = idx;
         j += draws >> 1;
-        if (++k == (uint32_t)a.spp) {  // the rest of the window belongs to this pixel: dropped
+        if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
             out[(size_t)(rs.row0 + r) * a.W + x] = pack_pixel(col, a.spp_recip);
             rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
             ++x;
             k = 0;
             pdraws = 0;
             col = mk(0.0f, 0.0f, 0.0f);
-            break;
+            if (wb != base || n2 == 0) break;
+            // on into the lookahead window, if the next pixel's first sample is in it
+            wb = base + n;
+            lo = s2;
+            hi = s2 + n2;
         }
     }
-    if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[base + last];  // the next sample's start state
+    if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[last];  // the next sample's start state
     if (k != 0) ++rs.short_win[r];
     rs.k[r] = k;
     rs.x[r] = x;
@@ -2165,7 +2186,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // the slowest row sets the iteration count)
     uint32_t wmax = (uint32_t)std::min<int64_t>(8192, std::max<int64_t>(64, (int64_t)a.spp * 24));
     if (const char* e = getenv("TMPT_ROWSPEC_WMAX")) wmax = (uint32_t)std::max(8, std::min(16384, atoi(e)));
-    float margin = 1.15f;  // window = expected draws x margin
+    float margin = 1.1f;  // window = expected draws x margin (1.05 / 1.1 / 1.15: 3.17 / 3.11 / 3.21 s)
     if (const char* e = getenv("TMPT_ROWSPEC_MARGIN")) margin = std::max(0.1f, (float)atof(e));
     int G = 2;  // row groups (streams)
     if (const char* e = getenv("TMPT_ROWSPEC_GROUPS")) G = atoi(e);
@@ -2179,9 +2200,16 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // smaller reservations balance the waves' loads)
     uint32_t chunk = kChunk;
     if (const char* e = getenv("TMPT_ROWSPEC_CHUNK")) chunk = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    if (s.jt2_n < (int32_t)wmax) {  // J_j = M^(2j): the state 2j draws on
+    // lookahead (a window of the next pixel, from look_lo of this one's
+    // expected end): about one iteration per two pixels
+    int look = 1;
+    if (const char* e = getenv("TMPT_ROWSPEC_LOOK")) look = atoi(e) != 0;
+    float look_lo = 0.9f;  // 0.75 / 0.85 / 0.9 / 0.95 at margin 1.15: 3.24 / 3.18 / 3.18 / 3.22 s
+    if (const char* e = getenv("TMPT_ROWSPEC_LO")) look_lo = std::max(0.0f, std::min(1.0f, (float)atof(e)));
+    const uint32_t jmax = 2 * wmax;  // offsets a unit may start at: both windows
+    if (s.jt2_n < (int32_t)jmax) {  // J_j = M^(2j): the state 2j draws on
         std::vector<uint32_t> tab;
-        jump_tables(2, (int32_t)wmax, tab);
+        jump_tables(2, (int32_t)jmax, tab);
         uint32_t* nt = nullptr;
         TMPT_HIP(hipMalloc(&nt, tab.size() * sizeof(uint32_t)));
         if (hipMemcpy(nt, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
@@ -2191,15 +2219,15 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         }
         if (s.jt2) (void)hipFree(s.jt2);
         s.jt2 = nt;
-        s.jt2_n = (int32_t)wmax;
+        s.jt2_n = (int32_t)jmax;
     }
     const size_t ovf_words = (size_t)pgrid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     auto group_rows = [&](int g) { return rows / G + (g < rows % G ? 1 : 0); };
     auto group_bytes = [&](int g) {
-        const size_t R = (size_t)group_rows(g), U = R * wmax;
-        return al(U * (sizeof(float4) + 3 * sizeof(uint32_t)) + R * sizeof(float4) + (10 * R + 2) * sizeof(uint32_t) +
+        const size_t R = (size_t)group_rows(g), U = R * jmax;
+        return al(U * (sizeof(float4) + 3 * sizeof(uint32_t)) + R * sizeof(float4) + (12 * R + 2) * sizeof(uint32_t) +
                   (ovf_words + head_words) * sizeof(uint32_t));
     };
     size_t need = al(24 * sizeof(unsigned long long));
@@ -2241,12 +2269,14 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         char* gp = p;
         p += group_bytes(g);
         const size_t R = (size_t)group_rows(g);
-        q.U = R * wmax;
+        q.U = R * jmax;
         q.st = s.rs_stream[g];
         q.rs.row0 = row0;
         q.rs.nrows = (int)R;
         q.rs.wmax = wmax;
         q.rs.margin = margin;
+        q.rs.look = look;
+        q.rs.look_lo = look_lo;
         row0 += (int)R;
         q.rs_out = reinterpret_cast<float4*>(gp);
         gp += q.U * sizeof(float4);
@@ -2258,7 +2288,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.rs_end = q.ustate + q.U;
         w = q.rs_end + q.U;
         uint32_t** fields[] = {&q.rs.rng, &q.rs.x, &q.rs.k, &q.rs.pdraws, &q.rs.prev_mean,
-                               &q.rs.rays, &q.rs.erays, &q.rs.win, &q.rs.short_win};
+                               &q.rs.rays, &q.rs.erays, &q.rs.win, &q.rs.short_win, &q.rs.win2, &q.rs.s2};
         for (uint32_t** f : fields) {
             *f = w;
             w += R;
