@@ -195,6 +195,8 @@ int tmpt_scene_destroy(tmpt_scene* h)
     Scene& s = h->s;
     (void)hipSetDevice(s.device);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (auto& st : s.rs_stream)  // the speculative row engine's group streams
+        if (st) (void)hipStreamSynchronize(st);
     if (s.nodes) (void)hipFree(s.nodes);
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.nodes4f) (void)hipFree(s.nodes4f);

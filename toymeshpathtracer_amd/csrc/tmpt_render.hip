@@ -2323,7 +2323,8 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     int it = 0;
     // every iteration moves each unfinished row by >= 1 sample, so W * spp bounds them
     const int64_t max_it = (int64_t)a.W * a.spp + kCheck;
-    for (bool done = false; !done && it < max_it;) {
+    bool done = false;
+    while (!done && it < max_it) {
         for (int c = 0; c < kCheck; ++c, ++it)
             for (Group& q : gs) {
                 k_rs_plan<<<1, 1024, 0, q.st>>>(a, q.rs);
@@ -2341,6 +2342,11 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
             TMPT_HIP(hipStreamSynchronize(gs[g].st));
             done = done && s.rs_host[g] == 0;
         }
+    }
+    if (!done) {  // cannot happen: every iteration moves each unfinished row on
+        set_error("render_rowspec: rows unfinished after " + std::to_string(it) + " iterations");
+        for (Group& q : gs) (void)hipStreamSynchronize(q.st);
+        return -1;
     }
     for (int g = 0; g < G; ++g) {
         k_rs_count<<<(unsigned)((gs[g].rs.nrows + 255) / 256), 256, 0, gs[g].st>>>(gs[g].rs, d_counters);
