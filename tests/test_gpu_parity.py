@@ -180,7 +180,9 @@ def test_row_mode_reproduces_reference_binary(gpu, name, engine):
 # ---------------------------------------------------------------- speculative row chains
 @pytest.mark.parametrize("env", [{}, {"TMPT_ROWSPEC_WMAX": "8"}, {"TMPT_ROWSPEC_WMAX": "33"},
                                  {"TMPT_ROWSPEC_LOOK": "0"}, {"TMPT_ROWSPEC_LOOK": "0", "TMPT_ROWSPEC_WMAX": "33"},
-                                 {"TMPT_ROWSPEC_LO": "0.3", "TMPT_ROWSPEC_MARGIN": "0.6"}])
+                                 {"TMPT_ROWSPEC_SPREAD": "0", "TMPT_ROWSPEC_LO": "0.3", "TMPT_ROWSPEC_MARGIN": "0.6"},
+                                 {"TMPT_ROWSPEC_SPREAD": "0.02", "TMPT_ROWSPEC_LOOK": "7"},
+                                 {"TMPT_ROWSPEC_SPREAD": "0"}])
 @pytest.mark.parametrize("name,w,h,spp", [("suzanne.obj", 320, 180, 16), ("teapot.obj", 203, 77, 7),
                                           ("cube.obj", 64, 1, 1), ("triangle.obj", 1, 3, 5)])
 def test_rowspec_equals_row_chains(gpu, monkeypatch, name, w, h, spp, env):

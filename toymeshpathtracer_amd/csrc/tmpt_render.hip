@@ -1308,22 +1308,26 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
 // chain through the window: take the sample at offset 0, add its colour in
 // sample order, jump to offset + its draws, ...  Each window costs ~draws/2
 // traces per chain sample (speculation), but all of them run in parallel.
+constexpr int kRsMaxWin = 8;  // windows per row and iteration: this pixel + up to 7 lookaheads
+
 struct RowSpec {
     int row0, nrows;  // this group's tile rows [row0, row0 + nrows)
     // per row of the group: chain state, current pixel and samples done in it,
     // its draws so far and the previous pixel's mean draws per sample (window
-    // sizing), chain rays (all, closest-hit), window, unit offsets (nrows + 1)
-    uint32_t *rng, *x, *k, *pdraws, *prev_mean, *rays, *erays, *win, *offs;
-    // lookahead window of the next pixel: offsets [s2, s2 + win2) (win2 = 0: none)
-    uint32_t *win2, *s2;
+    // sizing), chain rays (all, closest-hit), unit offsets (nrows + 1)
+    uint32_t *rng, *x, *k, *pdraws, *prev_mean, *rays, *erays, *offs;
+    // window i (pixel x + i) of row r: offsets [ws[i*nrows + r], + win[i*nrows + r]);
+    // window 0 starts at 0; win = 0: none
+    uint32_t *win, *ws;
     uint32_t* short_win;  // iterations whose window ended before the pixel did (diagnostic)
     float4* col;
     uint32_t* total;  // units of this iteration
     unsigned long long* planned;  // units over all iterations (diagnostic)
     uint32_t wmax;
     float margin;
-    float look_lo;  // lookahead window start, as a fraction of the current pixel's expected draws
-    int look;       // lookahead on
+    float look_lo;  // lookahead window start, as a fraction of the pixel's expected start
+    float spread;   // > 0: windows from expected positions +- spread * sqrt(i) pixels (default)
+    int nwin;       // windows per row (1 = no lookahead)
 };
 
 // Decode of a unit's rs_out.w: draws | rays << 23 | extend rays << 28.
@@ -1339,9 +1343,12 @@ __global__ void __launch_bounds__(256) k_rs_init(RenderArgs a, RowSpec rs)
     rs.col[r] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
-// Window per row: the remaining samples of its pixel at the larger of this
-// pixel's and the previous pixel's mean draws per sample, x margin, over 2
-// (even offsets only); exclusive scan into offs; total units.  One block.
+// Windows per row.  Window 0: the remaining samples of its pixel at the
+// larger of this pixel's and the previous pixel's mean draws per sample, x
+// margin, over 2 (even offsets only).  Lookahead window i: pixel x + i, from
+// look_lo of its expected start to one pixel's window past window i-1's end
+// (so the pixel can finish there if it starts anywhere in window i-1).
+// Exclusive scan into offs; total units.  One block.
 __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
 {
     __shared__ uint32_t part[1024];
@@ -1350,24 +1357,40 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     const int r0 = min(rows, (int)threadIdx.x * per), r1 = min(rows, r0 + per);
     uint32_t sum = 0;
     for (int r = r0; r < r1; ++r) {
-        uint32_t w = 0, w2 = 0, s2 = 0;
-        if (rs.x[r] < (uint32_t)a.W) {
+        const uint32_t x = rs.x[r];
+        uint32_t t = 0;  // end of the previous window
+        float mean = 0.0f, e0 = 0.0f, E = 0.0f;
+        if (x < (uint32_t)a.W) {
             const uint32_t k = rs.k[r];
-            float mean = __uint_as_float(rs.prev_mean[r]);
+            mean = __uint_as_float(rs.prev_mean[r]);
             if (k > 0) mean = fmaxf(mean, (float)rs.pdraws[r] / (float)k);
-            const float rem = (float)((uint32_t)a.spp - k);
-            w = min(rs.wmax, (uint32_t)(rem * mean * 0.5f * rs.margin) + 2u);
-            // lookahead: the next pixel from look_lo of this one's expected end
-            // through one pixel's window past this window's end
-            if (rs.look && rs.x[r] + 1u < (uint32_t)a.W) {
-                s2 = min(w, (uint32_t)(rem * mean * 0.5f * rs.look_lo));
-                w2 = min(rs.wmax, (w - s2) + (uint32_t)((float)a.spp * mean * 0.5f * rs.margin) + 2u);
-            }
+            e0 = (float)((uint32_t)a.spp - k) * mean * 0.5f;  // expected units to this pixel's end
+            E = (float)a.spp * mean * 0.5f;                   // ... of one whole pixel
         }
-        rs.win[r] = w;
-        rs.win2[r] = w2;
-        rs.s2[r] = s2;
-        sum += w + w2;
+        for (int i = 0; i < rs.nwin; ++i) {
+            uint32_t w = 0, s = 0;
+            if (x + (uint32_t)i < (uint32_t)a.W) {
+                if (rs.spread > 0.0f) {
+                    // pixel x + i starts near c_i = e0 + (i-1) E, give or take
+                    // spread * sqrt(i) * E; window i spans its start's and its
+                    // end's ranges
+                    const float ci = i == 0 ? 0.0f : e0 + (float)(i - 1) * E;
+                    const float ui = i == 0 ? 0.0f : rs.spread * sqrtf((float)i) * E;
+                    const float ce = e0 + (float)i * E, ue = rs.spread * sqrtf((float)(i + 1)) * E;
+                    s = i == 0 ? 0u : min(t, (uint32_t)fmaxf(0.0f, ci - ui));
+                    w = min(rs.wmax, (uint32_t)(ce + ue) + 2u - min(s, (uint32_t)(ce + ue)));
+                } else if (i == 0) {
+                    w = min(rs.wmax, (uint32_t)(e0 * rs.margin) + 2u);
+                } else {
+                    s = min(t, (uint32_t)((e0 + (float)(i - 1) * E) * rs.look_lo));
+                    w = min(rs.wmax, (t - s) + (uint32_t)(E * rs.margin) + 2u);
+                }
+                t = s + w;
+            }
+            rs.win[i * rows + r] = w;
+            rs.ws[i * rows + r] = s;
+            sum += w;
+        }
     }
     part[threadIdx.x] = sum;
     __syncthreads();
@@ -1380,7 +1403,7 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     uint32_t o = part[threadIdx.x] - sum;
     for (int r = r0; r < r1; ++r) {
         rs.offs[r] = o;
-        o += rs.win[r] + rs.win2[r];
+        for (int i = 0; i < rs.nwin; ++i) o += rs.win[i * rows + r];
     }
     if (threadIdx.x == 1023) {
         rs.offs[rows] = part[1023];
@@ -1389,8 +1412,9 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
     }
 }
 
-// Unit u -> (row, offset index j): pixel and start state M^(2j) rng[row].
-// Launched over the largest possible count; the plan's total bounds it.
+// Unit u -> (row, window i, offset index j): pixel x + i and start state
+// M^(2j) rng[row].  Launched over the largest possible count; the plan's
+// total bounds it.
 __global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const uint32_t* __restrict__ jt2,
                                                  uint32_t* __restrict__ upix, uint32_t* __restrict__ ustate)
 {
@@ -1402,30 +1426,32 @@ __global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const
         if (rs.offs[mid] <= u) lo = mid;
         else hi = mid - 1;
     }
-    const uint32_t l = u - rs.offs[lo], w = rs.win[lo];
-    const bool ahead = l >= w;  // the lookahead window: the next pixel
-    const uint32_t j = ahead ? rs.s2[lo] + (l - w) : l;
-    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo] + (ahead ? 1u : 0u);
+    uint32_t l = u - rs.offs[lo];
+    int i = 0;
+    for (; i + 1 < rs.nwin && l >= rs.win[i * rs.nrows + lo]; ++i) l -= rs.win[i * rs.nrows + lo];
+    const uint32_t j = rs.ws[i * rs.nrows + lo] + l;
+    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo] + (uint32_t)i;
     ustate[u] = sample_seed(jt2, j, rs.rng[lo]);
 }
 
 // The chase, one thread per row: the chain's samples in order through the
-// window (main.cpp:209-219), the pixel packed after its spp-th (:221-233).
+// windows (main.cpp:209-219), each pixel packed after its spp-th (:221-233);
+// on into window i + 1 when the next pixel's first sample falls in it.
 __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const float4* __restrict__ rs_out,
                                                  const uint32_t* __restrict__ rs_end, uint32_t* __restrict__ out)
 {
     const int r = blockIdx.x * 64 + threadIdx.x;
     if (r >= rs.nrows) return;
-    const uint32_t n = rs.win[r];
+    const int rows = rs.nrows;
+    uint32_t n = rs.win[r];
     if (n == 0) return;
-    const uint32_t base = rs.offs[r], n2 = rs.win2[r], s2 = rs.s2[r];
     uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
     const float4 c0 = rs.col[r];
     f3 col = mk(c0.x, c0.y, c0.z);
-    // window 0: this pixel, offsets [0, n) at base; window 1: the next pixel,
-    // offsets [s2, s2 + n2) at base + n
-    uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, hi = n, wb = base;
-    while (j >= lo && j < hi) {
+    // window i: offsets [lo, lo + n) at wb
+    uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, wb = rs.offs[r];
+    int i = 0;
+    while (j >= lo && j - lo < n) {
         const uint32_t idx = wb + (j - lo);
         const float4 t = rs_out[idx];
         const uint32_t w = __float_as_uint(t.w);
@@ -1443,11 +1469,11 @@ __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const
             k = 0;
             pdraws = 0;
             col = mk(0.0f, 0.0f, 0.0f);
-            if (wb != base || n2 == 0) break;
-            // on into the lookahead window, if the next pixel's first sample is in it
-            wb = base + n;
-            lo = s2;
-            hi = s2 + n2;
+            if (++i >= rs.nwin) break;
+            wb += n;
+            n = rs.win[i * rows + r];
+            lo = rs.ws[i * rows + r];
+            if (n == 0) break;
         }
     }
     if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[last];  // the next sample's start state
@@ -2200,13 +2226,18 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // smaller reservations balance the waves' loads)
     uint32_t chunk = kChunk;
     if (const char* e = getenv("TMPT_ROWSPEC_CHUNK")) chunk = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    // lookahead (a window of the next pixel, from look_lo of this one's
-    // expected end): about one iteration per two pixels
-    int look = 1;
-    if (const char* e = getenv("TMPT_ROWSPEC_LOOK")) look = atoi(e) != 0;
+    // lookahead windows (pixels x+1, x+2, ...; each from look_lo of its
+    // expected start): one iteration covers up to nwin pixels of a row.  The
+    // extra speculation is cheap while the GPU has room: nwin ~ 5 units per
+    // resident lane over the rows' expected pixel windows (~17 draws per
+    // sample), 2..kRsMaxWin -- 2 on the whole bench frame, 8 at 1/4 of it.
+    const int64_t lanes = (int64_t)pgrid * kBlk;
+    int nwin = (int)std::lround((double)lanes * 5.0 / ((double)rows * (double)a.spp * 8.5));
+    nwin = std::max(2, std::min(kRsMaxWin, nwin));
+    if (const char* e = getenv("TMPT_ROWSPEC_LOOK")) nwin = std::max(1, std::min(kRsMaxWin, atoi(e) + 1));
     float look_lo = 0.9f;  // 0.75 / 0.85 / 0.9 / 0.95 at margin 1.15: 3.24 / 3.18 / 3.18 / 3.22 s
     if (const char* e = getenv("TMPT_ROWSPEC_LO")) look_lo = std::max(0.0f, std::min(1.0f, (float)atof(e)));
-    const uint32_t jmax = 2 * wmax;  // offsets a unit may start at: both windows
+    const uint32_t jmax = (uint32_t)nwin * wmax;  // window i ends by (i + 1) * wmax
     if (s.jt2_n < (int32_t)jmax) {  // J_j = M^(2j): the state 2j draws on
         std::vector<uint32_t> tab;
         jump_tables(2, (int32_t)jmax, tab);
@@ -2227,7 +2258,8 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     auto group_rows = [&](int g) { return rows / G + (g < rows % G ? 1 : 0); };
     auto group_bytes = [&](int g) {
         const size_t R = (size_t)group_rows(g), U = R * jmax;
-        return al(U * (sizeof(float4) + 3 * sizeof(uint32_t)) + R * sizeof(float4) + (12 * R + 2) * sizeof(uint32_t) +
+        return al(U * (sizeof(float4) + 3 * sizeof(uint32_t)) + R * sizeof(float4) +
+                  ((9 + 2 * (size_t)kRsMaxWin) * R + 2) * sizeof(uint32_t) +
                   (ovf_words + head_words) * sizeof(uint32_t));
     };
     size_t need = al(24 * sizeof(unsigned long long));
@@ -2275,7 +2307,14 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.rs.nrows = (int)R;
         q.rs.wmax = wmax;
         q.rs.margin = margin;
-        q.rs.look = look;
+        q.rs.nwin = nwin;
+        // window placement: expected positions +- spread * sqrt(i) pixels;
+        // bench frame, 64 spp (profiles/r02_rowspec/rs15): spread 0.08 / 0.1 /
+        // 0.12 / 0.15 = 3.06 / 3.03 / 3.04 / 3.10 s whole, 0.85 / 0.74 / 0.69 /
+        // 0.67 s at 1/8 -- wider at low load, where speculation is cheap.
+        // TMPT_ROWSPEC_SPREAD=0: the linear placement (look_lo, margin)
+        q.rs.spread = 0.09f + 0.008f * (float)nwin;
+        if (const char* e = getenv("TMPT_ROWSPEC_SPREAD")) q.rs.spread = std::max(0.0f, (float)atof(e));
         q.rs.look_lo = look_lo;
         row0 += (int)R;
         q.rs_out = reinterpret_cast<float4*>(gp);
@@ -2288,11 +2327,15 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.rs_end = q.ustate + q.U;
         w = q.rs_end + q.U;
         uint32_t** fields[] = {&q.rs.rng, &q.rs.x, &q.rs.k, &q.rs.pdraws, &q.rs.prev_mean,
-                               &q.rs.rays, &q.rs.erays, &q.rs.win, &q.rs.short_win, &q.rs.win2, &q.rs.s2};
+                               &q.rs.rays, &q.rs.erays, &q.rs.short_win};
         for (uint32_t** f : fields) {
             *f = w;
             w += R;
         }
+        q.rs.win = w;  // kRsMaxWin x R each
+        w += kRsMaxWin * R;
+        q.rs.ws = w;
+        w += kRsMaxWin * R;
         q.rs.offs = w;  // rows + 1
         w += R + 1;
         q.rs.total = w;
