@@ -228,6 +228,9 @@ def main() -> None:
         for name, sd in seeds.items():
             if sd == seed:
                 continue
+            if name == "row" and W * H * SPP > 1920 * 1080 * 64:  # ~3 s per 1080p64 frame: skip larger ones
+                compare[name] = {"skipped": "frame larger than sponza1080 (row seeding ~3 s per 1080p 64 spp frame)"}
+                continue
             step(sd)
             if dist_on:
                 dist.barrier()
