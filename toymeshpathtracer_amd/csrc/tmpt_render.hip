@@ -1308,7 +1308,7 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
 // chain through the window: take the sample at offset 0, add its colour in
 // sample order, jump to offset + its draws, ...  Each window costs ~draws/2
 // traces per chain sample (speculation), but all of them run in parallel.
-constexpr int kRsMaxWin = 8;  // windows per row and iteration: this pixel + up to 7 lookaheads
+constexpr int kRsMaxWin = 32;  // windows per row and iteration: this pixel + up to 31 lookaheads
 
 struct RowSpec {
     int row0, nrows;  // this group's tile rows [row0, row0 + nrows)
@@ -2230,9 +2230,15 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // expected start): one iteration covers up to nwin pixels of a row.  The
     // extra speculation is cheap while the GPU has room: nwin ~ 5 units per
     // resident lane over the rows' expected pixel windows (~17 draws per
-    // sample), 2..kRsMaxWin -- 2 on the whole bench frame, 8 at 1/4 of it.
+    // sample), 2..kRsMaxWin -- 2 on the whole bench frame, 8 from 1/4 of it.
+    // The far windows' spread grows with a pixel's units E = spp x ~8.5, so
+    // the windows of one iteration are also capped at ~4400 units per row
+    // (8 windows at 64 spp).  Measured (profiles/r02_rowspec/rs16): 640x360x4
+    // suzanne 88 -> 51 ms with 8 -> 32 windows; the 1/8 shard of the bench
+    // frame 708 ms with 8 windows, 746 with 18.
     const int64_t lanes = (int64_t)pgrid * kBlk;
-    int nwin = (int)std::lround((double)lanes * 5.0 / ((double)rows * (double)a.spp * 8.5));
+    const double E_est = (double)a.spp * 8.5;
+    int nwin = (int)std::lround(std::min((double)lanes * 5.0 / ((double)rows * E_est), 4400.0 / E_est));
     nwin = std::max(2, std::min(kRsMaxWin, nwin));
     if (const char* e = getenv("TMPT_ROWSPEC_LOOK")) nwin = std::max(1, std::min(kRsMaxWin, atoi(e) + 1));
     float look_lo = 0.9f;  // 0.75 / 0.85 / 0.9 / 0.95 at margin 1.15: 3.24 / 3.18 / 3.18 / 3.22 s
