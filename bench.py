@@ -293,7 +293,9 @@ def main() -> None:
         achieved = b_ray * per_launch_rays / (avg_launch_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "kernel": "k_path (persistent: closest-hit + shadow queries + shading)",
+                "kernel": ("k_path (persistent: closest-hit + shadow queries + shading)" if args.seed_mode != "row" else
+                           "speculative row engine: k_path<SAMP=2> per iteration; reference-chain rays only "
+                           "(the speculative traces are ~13x as many)"),
                 **pmc_traffic(),
                 "bytes_per_ray": round(b_ray, 1), "n_node_per_ray": round(n_node, 2),
                 "n_tri_per_ray": round(n_tri, 2), "avg_launch_ms": round(avg_launch_ms, 4),
