@@ -227,6 +227,26 @@ def test_rowspec_shards_and_oracle(gpu):
     sc.close()
 
 
+def test_rowspec_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
+    """The bench frame at its full 64 spp in row seeding (the reference's own
+    RNG, each row one chain through 1920 x 64 samples): every 64th row equals
+    the oracle's row loop with the exact HitScene contract (lowest index on a
+    t tie).  Against the octree's visit-order ties (bench.py's parity_sample)
+    a tie changes one path's draws and with them the rest of its row's chain,
+    so those rows differ from that pixel on."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 64
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris) as sc:
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    assert rays == 1762408338
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_ROW, row_step=64, threads=16)
+    rows = np.arange(0, h, 64)
+    diff = np.nonzero((img[rows] != ref[rows]).any(-1))
+    assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+
+
 def test_rowspec_bench_frame_rows(gpu, sponza_path):
     """Bench workload (stand-in sponza 1920x1080) in row seeding at 2 spp: the
     speculative engine equals the megakernel's row chains on the whole frame."""
