@@ -2,8 +2,10 @@
 //   tmpt <width> <height> <spp> <objFile> [--seed row|pixel|sample] [--engine persistent|wavefront|mega]
 //        [--gpus N] [--device D] [--out output.png]
 // Defaults reproduce the reference: row seeding (main.cpp:204) and output.png.
-// Pixel or sample seeding is what the parallel engines need; row mode runs the
-// megakernel (one lane per row).  With --gpus N (tmpt_render_multi) the rows
+// Row seeding runs the speculative row engine on the persistent engine (every even RNG offset
+// of a window traced, the chain walked through it) and one lane per row with
+// --engine mega; pixel or sample seeding make every pixel or sample independent
+// work.  With --gpus N (tmpt_render_multi) the rows
 // are dealt round-robin one at a time (row y to device y % N), one host thread
 // per device, and the tiles are assembled into the frame.
 #include <stdio.h>
