@@ -182,7 +182,8 @@ def test_row_mode_reproduces_reference_binary(gpu, name, engine):
                                  {"TMPT_ROWSPEC_LOOK": "0"}, {"TMPT_ROWSPEC_LOOK": "0", "TMPT_ROWSPEC_WMAX": "33"},
                                  {"TMPT_ROWSPEC_SPREAD": "0", "TMPT_ROWSPEC_LO": "0.3", "TMPT_ROWSPEC_MARGIN": "0.6"},
                                  {"TMPT_ROWSPEC_SPREAD": "0.02", "TMPT_ROWSPEC_LOOK": "7"},
-                                 {"TMPT_ROWSPEC_SPREAD": "0"}])
+                                 {"TMPT_ROWSPEC_SPREAD": "0"}, {"TMPT_ROWSPEC_NOSHADOW": "0"},
+                                 {"TMPT_ROWSPEC_NOSHADOW": "0", "TMPT_ROWSPEC_WMAX": "8"}])
 @pytest.mark.parametrize("name,w,h,spp", [("suzanne.obj", 320, 180, 16), ("teapot.obj", 203, 77, 7),
                                           ("cube.obj", 64, 1, 1), ("triangle.obj", 1, 3, 5)])
 def test_rowspec_equals_row_chains(gpu, monkeypatch, name, w, h, spp, env):
@@ -247,16 +248,19 @@ def test_rowspec_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
     assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
 
 
-def test_rowspec_bench_frame_rows(gpu, sponza_path):
+def test_rowspec_bench_frame_rows(gpu, monkeypatch, sponza_path):
     """Bench workload (stand-in sponza 1920x1080) in row seeding at 2 spp: the
-    speculative engine equals the megakernel's row chains on the whole frame."""
+    speculative engine, with and without shadow-free speculation, equals the
+    megakernel's row chains on the whole frame."""
     tris, bmin, bmax = tm.load_scene(sponza_path)
     w, h, spp = 1920, 1080, 2
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
     with tm.Scene(tris) as sc:
         a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
         b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
-    assert ra == rb and np.array_equal(a, b)
+        monkeypatch.setenv("TMPT_ROWSPEC_NOSHADOW", "0")
+        c, rc = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    assert ra == rb == rc and np.array_equal(a, b) and np.array_equal(a, c)
 
 
 @pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL, tm.ENGINE_PERSISTENT])

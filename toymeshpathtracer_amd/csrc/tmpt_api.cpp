@@ -210,6 +210,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     for (auto& ev : s.rs_event)
         if (ev) (void)hipEventDestroy(ev);
     if (s.rs_host) (void)hipHostFree(s.rs_host);
+    if (s.rs_list) (void)hipFree(s.rs_list);
     free_shadow_grid(s);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);

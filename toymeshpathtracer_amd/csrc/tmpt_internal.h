@@ -143,6 +143,8 @@ struct Scene {
     hipStream_t rs_stream[kRowSpecMaxGroups] = {};      // one per row group
     hipEvent_t rs_event[kRowSpecMaxGroups + 1] = {};    // group ends; [max]: the start
     uint32_t* rs_host = nullptr;                        // pinned: each group's last unit count
+    void* rs_list = nullptr;                            // no-shadow speculation: the chain list
+    size_t rs_list_bytes = 0;
     int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
     hipEvent_t path_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // around the pilot / final k_path
     // statistics of the last render

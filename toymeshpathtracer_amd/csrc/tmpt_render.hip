@@ -641,6 +641,12 @@ struct PathCtl {
     float4* __restrict__ rs_out;
     uint32_t* __restrict__ rs_end;
     const uint32_t* __restrict__ p_dev;  // the unit count (replaces P, nchunks at launch)
+    // no-shadow speculation (TMPT_ROWSPEC_NOSHADOW): the speculative pass skips
+    // shadow traversals (they never change a sample's draws); the chain's
+    // samples are traced again in full at the end of the frame, unit u as
+    // sample uslot[u] of its pixel, colour into sbuf (resolved in order)
+    int rs_noshadow;
+    const uint32_t* __restrict__ uslot;
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -844,6 +850,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (SAMP == 2) {  // speculative row seeding: one sample from a given state
                         cur_unit = res + k;
                         pix = pc.upix[cur_unit];
+                        if (pc.uslot) smp0 = pc.uslot[cur_unit];
                         re0 = rays_e;
                         rs0 = rays_s;
                     } else if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
@@ -917,7 +924,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 nd = normalize(target - pos);
                         ++depth;
                         bool traced = false;
-                        if (lc > 0.0f && !(kFull && pc.diag_noshadow)) {
+                        if (lc > 0.0f && !(kFull && pc.diag_noshadow) && !(SAMP == 2 && pc.rs_noshadow)) {
                             // shadow query: with the light-space grid, the triangles of
                             // the origin's cell (one leaf range, tested by the leaf
                             // steps of the traversal rounds); without, the BVH
@@ -1006,7 +1013,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (!pend) {
                     for (int kk = (int)depth - 1; kk >= 0; --kk)
                         color = backward_step(color, light[kk * BLOCK]);
-                    if (SAMP == 2) {  // speculative row seeding: render_rowspec's chase consumes it
+                    if (SAMP == 2 && pc.sbuf) {  // a chain sample traced in full: k_resolve sums in order
+                        typedef float f32x4 __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
+                                                    reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss +
+                                                                                        (size_t)pix * pc.sb_sp)));
+                    } else if (SAMP == 2) {  // speculative row seeding: render_rowspec's chase consumes it
                         // draws: the camera's, and RandomUnitVector's 2 at each of the
                         // `depth` hits (main.cpp:71, drawn at the 10th hit too)
                         const uint32_t draws = ndraw + 2u * depth;
@@ -1328,6 +1340,12 @@ struct RowSpec {
     float look_lo;  // lookahead window start, as a fraction of the pixel's expected start
     float spread;   // > 0: windows from expected positions +- spread * sqrt(i) pixels (default)
     int nwin;       // windows per row (1 = no lookahead)
+    // no-shadow speculation: the chase lists the chain's samples (tile pixel,
+    // start state, sample index) for the full re-trace; scratch holds a row's
+    // (unit, sample index) pairs of one iteration (scap per row)
+    uint32_t *lpix, *lstate, *lslot, *lcount;
+    uint2* scratch;
+    uint32_t scap;
 };
 
 // Decode of a unit's rs_out.w: draws | rays << 23 | extend rays << 28.
@@ -1438,52 +1456,71 @@ __global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const
 // windows (main.cpp:209-219), each pixel packed after its spp-th (:221-233);
 // on into window i + 1 when the next pixel's first sample falls in it.
 __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const float4* __restrict__ rs_out,
-                                                 const uint32_t* __restrict__ rs_end, uint32_t* __restrict__ out)
+                                                 const uint32_t* __restrict__ rs_end, uint32_t* __restrict__ out,
+                                                 const uint32_t* __restrict__ upix, const uint32_t* __restrict__ ustate)
 {
     const int r = blockIdx.x * 64 + threadIdx.x;
-    if (r >= rs.nrows) return;
     const int rows = rs.nrows;
-    uint32_t n = rs.win[r];
-    if (n == 0) return;
-    uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
-    const float4 c0 = rs.col[r];
-    f3 col = mk(c0.x, c0.y, c0.z);
-    // window i: offsets [lo, lo + n) at wb
-    uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, wb = rs.offs[r];
-    int i = 0;
-    while (j >= lo && j - lo < n) {
-        const uint32_t idx = wb + (j - lo);
-        const float4 t = rs_out[idx];
-        const uint32_t w = __float_as_uint(t.w);
-        const uint32_t draws = w & ((1u << kRsDrawBits) - 1u);
-        rays += (w >> kRsDrawBits) & 31u;
-        erays += w >> 28;
-        pdraws += draws;
-        col = col + mk(t.x, t.y, t.z);  // col += Trace(...), main.cpp:218
-        last = idx;
-        j += draws >> 1;
-        if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
-            out[(size_t)(rs.row0 + r) * a.W + x] = pack_pixel(col, a.spp_recip);
-            rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
-            ++x;
-            k = 0;
-            pdraws = 0;
-            col = mk(0.0f, 0.0f, 0.0f);
-            if (++i >= rs.nwin) break;
-            wb += n;
-            n = rs.win[i * rows + r];
-            lo = rs.ws[i * rows + r];
-            if (n == 0) break;
+    const bool listing = rs.lpix != nullptr;  // no-shadow speculation: list the chain, no colours
+    uint32_t n = r < rows ? rs.win[r] : 0u, nl = 0;
+    if (n > 0) {
+        uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
+        const float4 c0 = rs.col[r];
+        f3 col = mk(c0.x, c0.y, c0.z);
+        // window i: offsets [lo, lo + n) at wb
+        uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, wb = rs.offs[r];
+        int i = 0;
+        while (j >= lo && j - lo < n) {
+            const uint32_t idx = wb + (j - lo);
+            const float4 t = rs_out[idx];
+            const uint32_t w = __float_as_uint(t.w);
+            const uint32_t draws = w & ((1u << kRsDrawBits) - 1u);
+            rays += (w >> kRsDrawBits) & 31u;
+            erays += w >> 28;
+            pdraws += draws;
+            if (listing) rs.scratch[(size_t)r * rs.scap + nl++] = make_uint2(idx, k);
+            else col = col + mk(t.x, t.y, t.z);  // col += Trace(...), main.cpp:218
+            last = idx;
+            j += draws >> 1;
+            if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
+                if (!listing) out[(size_t)(rs.row0 + r) * a.W + x] = pack_pixel(col, a.spp_recip);
+                rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
+                ++x;
+                k = 0;
+                pdraws = 0;
+                col = mk(0.0f, 0.0f, 0.0f);
+                if (++i >= rs.nwin) break;
+                wb += n;
+                n = rs.win[i * rows + r];
+                lo = rs.ws[i * rows + r];
+                if (n == 0) break;
+            }
         }
+        if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[last];  // the next sample's start state
+        if (k != 0) ++rs.short_win[r];
+        rs.k[r] = k;
+        rs.x[r] = x;
+        rs.pdraws[r] = pdraws;
+        rs.rays[r] = rays;
+        rs.erays[r] = erays;
+        rs.col[r] = make_float4(col.x, col.y, col.z, 0.0f);
     }
-    if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[last];  // the next sample's start state
-    if (k != 0) ++rs.short_win[r];
-    rs.k[r] = k;
-    rs.x[r] = x;
-    rs.pdraws[r] = pdraws;
-    rs.rays[r] = rays;
-    rs.erays[r] = erays;
-    rs.col[r] = make_float4(col.x, col.y, col.z, 0.0f);
+    if (!listing) return;
+    // the row's chain samples into the frame's list: one atomic per wave
+    uint32_t incl = nl;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+        if ((threadIdx.x & 63) >= (unsigned)off) incl += v;
+    }
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 63) base = atomicAdd(rs.lcount, incl);
+    base = (uint32_t)__shfl((int)base, 63) + incl - nl;
+    for (uint32_t t = 0; t < nl; ++t) {
+        const uint2 e = rs.scratch[(size_t)r * rs.scap + t];
+        rs.lpix[base + t] = upix[e.x];
+        rs.lstate[base + t] = ustate[e.x];
+        rs.lslot[base + t] = e.y;
+    }
 }
 
 // The chain's rays (the reference's count): counters[0] all, [3] closest-hit.
@@ -2244,6 +2281,50 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     float look_lo = 0.9f;  // 0.75 / 0.85 / 0.9 / 0.95 at margin 1.15: 3.24 / 3.18 / 3.18 / 3.22 s
     if (const char* e = getenv("TMPT_ROWSPEC_LO")) look_lo = std::max(0.0f, std::min(1.0f, (float)atof(e)));
     const uint32_t jmax = (uint32_t)nwin * wmax;  // window i ends by (i + 1) * wmax
+    // Speculate without shadow traversals and re-trace the chain in full at the
+    // end (the frame's chain list and colour buffer must fit; else the colours
+    // come from the speculative pass).  Bench frame 3.03 -> 2.49 s, 1/8 shard
+    // 0.71 -> 0.61 s (profiles/r02_rowspec/rs19).  TMPT_ROWSPEC_NOSHADOW=0: off
+    bool noshadow = true;
+    if (const char* e = getenv("TMPT_ROWSPEC_NOSHADOW")) noshadow = atoi(e) != 0;
+    const size_t lcap = (size_t)a.slots * (size_t)a.spp;  // chain samples of the tile
+    const uint32_t scap = (uint32_t)nwin * (uint32_t)a.spp;  // a row's chain samples per iteration
+    if (noshadow) {
+        const size_t lneed = lcap * 3 * sizeof(uint32_t) + (size_t)rows * scap * sizeof(uint2) + 256;
+        const size_t sneed = lcap * sizeof(float4);
+        size_t fr = 0, tot = 0;
+        const size_t budget = (hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0) + s.rs_list_bytes + s.sbuf_bytes;
+        if (lcap >= (1ull << 32) || lneed + sneed > budget) {
+            noshadow = false;  // does not fit: the colours come from the speculative pass
+        } else {
+            if (s.rs_list_bytes < lneed) {
+                if (s.rs_list) (void)hipFree(s.rs_list);
+                s.rs_list = nullptr;
+                s.rs_list_bytes = 0;
+                TMPT_HIP(hipMalloc(&s.rs_list, lneed));
+                s.rs_list_bytes = lneed;
+            }
+            if (s.sbuf_bytes < sneed) {
+                if (s.sbuf) (void)hipFree(s.sbuf);
+                s.sbuf = nullptr;
+                s.sbuf_bytes = 0;
+                TMPT_HIP(hipMalloc(&s.sbuf, sneed));
+                s.sbuf_bytes = sneed;
+            }
+        }
+    }
+    uint32_t* lpix = nullptr;
+    uint32_t* lstate = nullptr;
+    uint32_t* lslot = nullptr;
+    uint32_t* lcount = nullptr;
+    uint2* scratch = nullptr;
+    if (noshadow) {
+        lcount = static_cast<uint32_t*>(s.rs_list);
+        scratch = reinterpret_cast<uint2*>(static_cast<char*>(s.rs_list) + 256);
+        lpix = reinterpret_cast<uint32_t*>(scratch + (size_t)rows * scap);
+        lstate = lpix + lcap;
+        lslot = lstate + lcap;
+    }
     if (s.jt2_n < (int32_t)jmax) {  // J_j = M^(2j): the state 2j draws on
         std::vector<uint32_t> tab;
         jump_tables(2, (int32_t)jmax, tab);
@@ -2358,11 +2439,19 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.pc.rs_out = q.rs_out;
         q.pc.rs_end = q.rs_end;
         q.pc.p_dev = q.rs.total;
+        q.pc.rs_noshadow = noshadow ? 1 : 0;
+        q.rs.lpix = lpix;
+        q.rs.lstate = lstate;
+        q.rs.lslot = lslot;
+        q.rs.lcount = lcount;
+        q.rs.scratch = scratch ? scratch + (size_t)q.rs.row0 * scap : nullptr;
+        q.rs.scap = scap;
         q.rs.planned = spec_ctr + 8;
     }
     // the groups start after the work already on the scene's stream (the
     // caller's wait), and that stream resumes after all of them
     TMPT_HIP(hipMemsetAsync(spec_ctr, 0, 24 * sizeof(unsigned long long), s.stream));
+    if (noshadow) TMPT_HIP(hipMemsetAsync(lcount, 0, 4, s.stream));
     TMPT_HIP(hipEventRecord(s.rs_event[kRowSpecMaxGroups], s.stream));
     for (Group& q : gs) {
         TMPT_HIP(hipStreamWaitEvent(q.st, s.rs_event[kRowSpecMaxGroups], 0));
@@ -2380,7 +2469,8 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
                 k_rs_fill<<<(unsigned)((q.U + 255) / 256), 256, 0, q.st>>>(a, q.rs, s.jt2, q.upix, q.ustate);
                 TMPT_HIP(hipMemsetAsync(q.heads, 0, head_words * 4, q.st));
                 fn<<<pgrid, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
-                k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, d_out);
+                k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, d_out,
+                                                                                q.upix, q.ustate);
             }
         TMPT_HIP(hipGetLastError());
         // the last plan of each group: 0 units = the group was already done
@@ -2403,6 +2493,22 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         TMPT_HIP(hipStreamWaitEvent(s.stream, s.rs_event[g], 0));
     }
     TMPT_HIP(hipGetLastError());
+    if (noshadow) {  // the chain's samples in full (shadows included), then the in-order sums
+        PathCtl pc2 = gs[0].pc;
+        pc2.upix = lpix;
+        pc2.ustate = lstate;
+        pc2.uslot = lslot;
+        pc2.p_dev = lcount;
+        pc2.rs_noshadow = 0;
+        pc2.sbuf = s.sbuf;
+        pc2.sb_ss = 1u;
+        pc2.sb_sp = (uint32_t)a.spp;
+        pc2.sb_nt = 1;
+        TMPT_HIP(hipMemsetAsync(gs[0].heads, 0, head_words * 4, s.stream));
+        fn<<<pgrid, kBlk, 0, s.stream>>>(view(s), as, pc2, d_out, gs[0].ovf, spec_ctr + 16);
+        k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(s.sbuf, a.slots, a.spp, a.spp_recip, d_out);
+        TMPT_HIP(hipGetLastError());
+    }
     s.path_launches = it;
     if (getenv("TMPT_ROWSPEC_LOG")) {
         unsigned long long c[2] = {0, 0};
