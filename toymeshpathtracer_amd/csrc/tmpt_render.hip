@@ -2400,7 +2400,9 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         // 0.12 / 0.15 = 3.06 / 3.03 / 3.04 / 3.10 s whole, 0.85 / 0.74 / 0.69 /
         // 0.67 s at 1/8 -- wider at low load, where speculation is cheap.
         // TMPT_ROWSPEC_SPREAD=0: the linear placement (look_lo, margin)
-        q.rs.spread = 0.09f + 0.008f * (float)nwin;
+        // (with shadow-free speculation: 1/8 shard spread 0.154 / 0.2 = 640 / 576 ms,
+        // whole frame 0.106 / 0.14 / 0.2 = 2.51 / 2.52 / 2.62 s, rs20)
+        q.rs.spread = 0.07f + 0.016f * (float)nwin;
         if (const char* e = getenv("TMPT_ROWSPEC_SPREAD")) q.rs.spread = std::max(0.0f, (float)atof(e));
         q.rs.look_lo = look_lo;
         row0 += (int)R;
