@@ -284,3 +284,75 @@ def test_sample_mode_first_sample_is_pixel_mode():
     a, _ = sc.render(cam, 80, 45, 4, seed_mode=oracle.SEED_SAMPLE)
     b, _ = sc.render(cam, 80, 45, 4, seed_mode=oracle.SEED_PIXEL)
     assert not np.array_equal(a, b)
+
+
+def _sample_from_state(sc, cam, x, y, w, h, st):
+    """One camera sample of main.cpp:212-218 from RNG state st, over the
+    oracle's pinned primitives: (colour, end state, rays)."""
+    inv_w, inv_h = np.float32(1) / np.float32(w), np.float32(1) / np.float32(h)
+    jx, jy = oracle.float01_seq(st, 2)
+    st = int(oracle.xorshift_seq(st, 2)[-1])
+    o, d, st = oracle.get_ray(cam, float((np.float32(x) + jx) * inv_w), float((np.float32(y) + jy) * inv_h), st)
+    return sc.trace(o, d, st)
+
+
+def test_speculative_row_chains_restated():
+    """The speculative row engine's method (tmpt_render.hip render_rowspec),
+    restated in Python over the oracle's primitives: per row and iteration,
+    trace one sample at EVERY even RNG offset of a window (and of a lookahead
+    window for the next pixel), then walk the chain through them.  The image
+    and ray count equal the oracle's row-seeded loop (main.cpp:202-233, the
+    reference's own RNG), and every sample takes an even number of draws --
+    the fact the method rests on.  Small windows force chains that leave a
+    window mid-pixel and next pixels that start outside the lookahead."""
+    tris, bmin, bmax = oracle.load_scene(data("suzanne.obj"))
+    w, h, spp = 9, 4, 3
+    cam = oracle.camera_for_scene(bmin, bmax, w, h)
+    sc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX)
+    ref, ref_rays = sc.render(cam, w, h, spp, seed_mode=oracle.SEED_ROW)
+    img = np.zeros_like(ref)
+    total = 0
+    recip = np.float32(1) / np.float32(spp)
+    cache = {}
+
+    def unit(x, y, st):  # (colour, draws, end state, rays) of the sample starting at st
+        key = (x, y, st)
+        if key not in cache:
+            c, end, r = _sample_from_state(sc, cam, x, y, w, h, st)
+            draws = 1
+            s = int(oracle.xorshift_seq(st, 1)[-1])
+            while s != end:
+                s = int(oracle.xorshift_seq(s, 1)[-1])
+                draws += 1
+                assert draws < 10000
+            assert draws % 2 == 0
+            cache[key] = (c, draws, end, r)
+        return cache[key]
+
+    for y in range(h):
+        st = y * 9781 + 1  # main.cpp:204
+        x, k, col = 0, 0, np.zeros(3, np.float32)
+        while x < w:
+            # windows (offset start, count) for pixels x and x + 1, in units of 2 draws
+            wins = [(0, 5), (3, 12)] if x + 1 < w else [(0, 5)]
+            units = [[unit(x + i, y, oracle.xorshift_jump(st, 2 * (s0 + j))) for j in range(n)]
+                     for i, (s0, n) in enumerate(wins)]
+            j, i, last = 0, 0, None
+            while wins[i][0] <= j < wins[i][0] + wins[i][1]:
+                c, draws, end, r = units[i][j - wins[i][0]]
+                col = col + c
+                total += r
+                last = end
+                j += draws // 2
+                k += 1
+                if k == spp:
+                    v = np.sqrt(col * recip)
+                    img[y, x, :3] = (np.minimum(np.maximum(v, 0), 1) * np.float32(255)).astype(np.uint8)
+                    img[y, x, 3] = 255
+                    x, k, col = x + 1, 0, np.zeros(3, np.float32)
+                    i += 1
+                    if i >= len(wins):
+                        break
+            st = last  # the next sample's start state
+    assert total == ref_rays
+    assert np.array_equal(img, ref)
