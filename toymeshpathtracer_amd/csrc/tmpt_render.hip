@@ -688,8 +688,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                                                 unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
-    __shared__ float s_light[kMaxDepth * BLOCK];
-    __shared__ float s_next[6 * BLOCK];
+    // SAMP 3 (shadow-free speculation): no light terms, no pending next ray
+    __shared__ float s_light[SAMP == 3 ? 1 : kMaxDepth * BLOCK];
+    __shared__ float s_next[SAMP == 3 ? 1 : 6 * BLOCK];
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     float* light = &s_light[threadIdx.x];
@@ -725,7 +726,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
     uint32_t res = 0, res_end = 0;
-    if (SAMP == 2) {  // the speculative row engine plans its units on the device
+    if (SAMP >= 2) {  // the speculative row engine plans its units on the device
         pc.P = *pc.p_dev;
         pc.nchunks = (uint32_t)((pc.P + pc.chunk - 1) / pc.chunk);
     }
@@ -847,7 +848,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
                     uint32_t smp0 = (uint32_t)a.smp_begin;
-                    if (SAMP == 2) {  // speculative row seeding: one sample from a given state
+                    if (SAMP >= 2) {  // speculative row seeding: one sample from a given state
                         cur_unit = res + k;
                         pix = pc.upix[cur_unit];
                         if (pc.uslot) smp0 = pc.uslot[cur_unit];
@@ -869,7 +870,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                    if (SAMP == 2) {
+                    if (SAMP >= 2) {
                         rng = pc.ustate[cur_unit];
                     } else if (!kFull || a.smp_begin == 0) {
                         rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
@@ -919,12 +920,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const f3 pos = hit_pos(mk(ha.x, ha.y, ha.z), mk(ha.w, hb.x, hb.y), mk(hb.z, hb.w, hc.x),
                                                ts.bu, ts.bv);
                         const float lc = light_cosine(nrm, r.d);
-                        light[depth * BLOCK] = lc;  // zeroed if occluded
+                        if (SAMP != 3) light[depth * BLOCK] = lc;  // zeroed if occluded
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
                         bool traced = false;
-                        if (lc > 0.0f && !(kFull && pc.diag_noshadow) && !(SAMP == 2 && pc.rs_noshadow)) {
+                        if (SAMP != 3 && lc > 0.0f && !(kFull && pc.diag_noshadow) && !(SAMP == 2 && pc.rs_noshadow)) {
                             // shadow query: with the light-space grid, the triangles of
                             // the origin's cell (one leaf range, tested by the leaf
                             // steps of the traversal rounds); without, the BVH
@@ -959,7 +960,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         color = sky(r.d);  // main.cpp:106-107
                         finish = true;
                     }
-                } else {  // shadow query of bounce depth-1
+                } else if (SAMP != 3) {  // shadow query of bounce depth-1
                     if (ts.best >= 0) light[(depth - 1) * BLOCK] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
                         start = true;  // the scattered ray of that bounce
@@ -1011,20 +1012,23 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     for (int kk = 0; kk < (int)depth; ++kk) pend |= light[kk * BLOCK] < 0.0f;
                 waiting = pend;
                 if (!pend) {
-                    for (int kk = (int)depth - 1; kk >= 0; --kk)
-                        color = backward_step(color, light[kk * BLOCK]);
+                    if (SAMP != 3)
+                        for (int kk = (int)depth - 1; kk >= 0; --kk)
+                            color = backward_step(color, light[kk * BLOCK]);
                     if (SAMP == 2 && pc.sbuf) {  // a chain sample traced in full: k_resolve sums in order
                         typedef float f32x4 __attribute__((ext_vector_type(4)));
                         __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
                                                     reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss +
                                                                                         (size_t)pix * pc.sb_sp)));
-                    } else if (SAMP == 2) {  // speculative row seeding: render_rowspec's chase consumes it
+                    } else if (SAMP >= 2) {  // speculative row seeding: render_rowspec's chase consumes it
                         // draws: the camera's, and RandomUnitVector's 2 at each of the
                         // `depth` hits (main.cpp:71, drawn at the 10th hit too)
                         const uint32_t draws = ndraw + 2u * depth;
                         const uint32_t ne = rays_e - re0, nr = ne + rays_s - rs0;  // <= 10, <= 20
+                        // SAMP 3 (the shadow-free pass): no colour, the chain is traced again
                         pc.rs_out[cur_unit] =
-                            make_float4(color.x, color.y, color.z, __uint_as_float(draws | (nr << 23) | (ne << 28)));
+                            make_float4(SAMP == 3 ? 0.0f : color.x, SAMP == 3 ? 0.0f : color.y, SAMP == 3 ? 0.0f : color.z,
+                                        __uint_as_float(draws | (nr << 23) | (ne << 28)));
                         pc.rs_end[cur_unit] = rng;
                     } else if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve sums in sample order
                         float4* dst = pc.sbuf + ((size_t)smp * pc.sb_ss + (size_t)pix * pc.sb_sp);
@@ -1054,7 +1058,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             pc.tlog[4 * (size_t)pix + 3] = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) |
                                                            (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu);
                         }
-                        if (SAMP != 2 && (!SAMP || !pc.sbuf))
+                        if (SAMP < 2 && (!SAMP || !pc.sbuf))
                             out[pix] = (COUNT && pc.cost_map)
                                            ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
                                                                : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
@@ -1087,7 +1091,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     pf_smp = more ? smp + 1u : 0xFFFFFFFFu;
                     pf_pix = pix;
                 }
-                if (SAMP == 2) {
+                if (SAMP >= 2) {
                     ndraw = 0;
                     camera_sample(a.cam, (uint32_t)x, y, a.invW, a.invH, rng, so, sd, ndraw);
                 } else {
@@ -1320,6 +1324,7 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
 // chain through the window: take the sample at offset 0, add its colour in
 // sample order, jump to offset + its draws, ...  Each window costs ~draws/2
 // traces per chain sample (speculation), but all of them run in parallel.
+constexpr int kRsOcc3 = 5;  // blocks per CU of the shadow-free pass (5 waves per SIMD)
 constexpr int kRsMaxWin = 32;  // windows per row and iteration: this pixel + up to 31 lookaheads
 
 struct RowSpec {
@@ -2241,7 +2246,11 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
 {
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2, kCheck = 64;
     auto fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 2>;
+    // the shadow-free pass: its own instantiation (no shadow, light or colour
+    // code, no light / next-ray LDS)
+    auto fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, kRsOcc3, kSparse, 0, 0, 3>;
     const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const int grid3 = occupancy_grid((const void*)fn3, kBlk, 0, s.device);
     const int rows = a.tile_rows;
     // window cap: one iteration covers a pixel's samples at up to 2 * wmax / spp
     // = 48 draws per sample (the stand-in sponza averages ~17, its deepest rows
@@ -2259,6 +2268,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     int gdiv = 1;
     if (const char* e = getenv("TMPT_ROWSPEC_GDIV")) gdiv = std::max(1, std::min(16, atoi(e)));
     const int pgrid = std::max(1, grid / gdiv);
+    const int pgrid3 = std::max(1, grid3 / gdiv);
     // units a wave reserves at once (a launch holds ~1.5 units per lane, so
     // smaller reservations balance the waves' loads)
     uint32_t chunk = kChunk;
@@ -2339,7 +2349,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         s.jt2 = nt;
         s.jt2_n = (int32_t)jmax;
     }
-    const size_t ovf_words = (size_t)pgrid * kBlk * (kStackTotal - kPathSL);
+    const size_t ovf_words = (size_t)std::max(pgrid, pgrid3) * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     auto group_rows = [&](int g) { return rows / G + (g < rows % G ? 1 : 0); };
@@ -2470,7 +2480,8 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
                 k_rs_plan<<<1, 1024, 0, q.st>>>(a, q.rs);
                 k_rs_fill<<<(unsigned)((q.U + 255) / 256), 256, 0, q.st>>>(a, q.rs, s.jt2, q.upix, q.ustate);
                 TMPT_HIP(hipMemsetAsync(q.heads, 0, head_words * 4, q.st));
-                fn<<<pgrid, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
+                if (noshadow) fn3<<<pgrid3, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
+                else fn<<<pgrid, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
                 k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, d_out,
                                                                                 q.upix, q.ustate);
             }
