@@ -18,7 +18,7 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-KEYS = ("TMPT_ROWSPEC_GROUPS", "TMPT_ROWSPEC_MARGIN", "TMPT_ROWSPEC_WMAX", "TMPT_ROWSPEC", "TMPT_ROWSPEC_GDIV", "TMPT_ROWSPEC_CHUNK", "TMPT_ROWSPEC_LOOK", "TMPT_ROWSPEC_LO", "TMPT_ROWSPEC_SPREAD", "TMPT_ROWSPEC_NOSHADOW")
+KEYS = ("TMPT_ROWSPEC_GROUPS", "TMPT_ROWSPEC_MARGIN", "TMPT_ROWSPEC_WMAX", "TMPT_ROWSPEC", "TMPT_ROWSPEC_GDIV", "TMPT_ROWSPEC_CHUNK", "TMPT_ROWSPEC_LOOK", "TMPT_ROWSPEC_LO", "TMPT_ROWSPEC_SPREAD", "TMPT_ROWSPEC_NOSHADOW", "TMPT_ROWSPEC_OCC")
 
 
 def main():

@@ -2249,6 +2249,8 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // the shadow-free pass: its own instantiation (no shadow, light or colour
     // code, no light / next-ray LDS)
     auto fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, kRsOcc3, kSparse, 0, 0, 3>;
+    if (const char* e = getenv("TMPT_ROWSPEC_OCC"))  // A/B: 6 waves per SIMD (80 VGPRs, 21 spilled dwords)
+        if (atoi(e) == 6) fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 6, kSparse, 0, 0, 3>;
     const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     const int grid3 = occupancy_grid((const void*)fn3, kBlk, 0, s.device);
     const int rows = a.tile_rows;
