@@ -21,7 +21,7 @@ import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
 BUILD_KEYS = ("TMPT_TREELET", "TMPT_TREELET_MIN", "TMPT_LAYOUT", "TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
-RENDER_KEYS = ("TMPT_SAMPLE_BLOCK", "TMPT_SBUF", "TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
+RENDER_KEYS = ("TMPT_SAMPLE_OCC", "TMPT_SAMPLE_BLOCK", "TMPT_SBUF", "TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]

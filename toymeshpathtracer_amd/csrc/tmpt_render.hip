@@ -647,6 +647,10 @@ struct PathCtl {
     // sample uslot[u] of its pixel, colour into sbuf (resolved in order)
     int rs_noshadow;
     const uint32_t* __restrict__ uslot;
+    // sample kernel at 5 waves per SIMD (OCC 5, A/B): light terms and the
+    // pending scattered ray per lane in global memory, [k][lane] (LDS holds
+    // only the stack and the top nodes)
+    float* __restrict__ gl_store;
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -689,12 +693,14 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
     // SAMP 3 (shadow-free speculation): no light terms, no pending next ray
-    __shared__ float s_light[SAMP == 3 ? 1 : kMaxDepth * BLOCK];
-    __shared__ float s_next[SAMP == 3 ? 1 : 6 * BLOCK];
+    constexpr bool kGL = SAMP == 1 && OCC >= 5;
+    __shared__ float s_light[(SAMP == 3 || kGL) ? 1 : kMaxDepth * BLOCK];
+    __shared__ float s_next[(SAMP == 3 || kGL) ? 1 : 6 * BLOCK];
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
-    float* light = &s_light[threadIdx.x];
-    float* nxt = &s_next[threadIdx.x];
+    const uint32_t LS = kGL ? gridDim.x * BLOCK : BLOCK;  // stride between a lane's entries
+    float* light = kGL ? pc.gl_store + gtid : &s_light[threadIdx.x];
+    float* nxt = kGL ? pc.gl_store + (size_t)kMaxDepth * LS + gtid : &s_next[threadIdx.x];
     // HELP: lane ids of this round's offloading lanes, by rank (per wave)
     __shared__ uint8_t s_pair[HELP ? BLOCK : 1];
     if (FMT == 4) {  // the top BVH4 levels (nodes are numbered level by level) in LDS
@@ -920,7 +926,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const f3 pos = hit_pos(mk(ha.x, ha.y, ha.z), mk(ha.w, hb.x, hb.y), mk(hb.z, hb.w, hc.x),
                                                ts.bu, ts.bv);
                         const float lc = light_cosine(nrm, r.d);
-                        if (SAMP != 3) light[depth * BLOCK] = lc;  // zeroed if occluded
+                        if (SAMP != 3) light[depth * LS] = lc;  // zeroed if occluded
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
@@ -932,8 +938,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             const bool grid = kFull && sv.sg.R > 0;
                             if (grid) gcell = shadow_grid_cell(sv, pos);
                             if (!grid || gcell.y != 0) {
-                                nxt[0] = pos.x; nxt[BLOCK] = pos.y; nxt[2 * BLOCK] = pos.z;
-                                nxt[3 * BLOCK] = nd.x; nxt[4 * BLOCK] = nd.y; nxt[5 * BLOCK] = nd.z;
+                                nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
+                                nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
                                 start = true;  // shadow query toward the light
                                 sany = true;
                                 so = pos;
@@ -961,11 +967,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         finish = true;
                     }
                 } else if (SAMP != 3) {  // shadow query of bounce depth-1
-                    if (ts.best >= 0) light[(depth - 1) * BLOCK] = 0.0f;
+                    if (ts.best >= 0) light[(depth - 1) * LS] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
                         start = true;  // the scattered ray of that bounce
-                        so = mk(nxt[0], nxt[BLOCK], nxt[2 * BLOCK]);
-                        sd = mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]);
+                        so = mk(nxt[0], nxt[LS], nxt[2 * LS]);
+                        sd = mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
                     } else {
                         finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
                     }
@@ -987,10 +993,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     const float hx = __shfl(so.x, src), hy = __shfl(so.y, src), hz = __shfl(so.z, src);
                     const uint32_t hs = (uint32_t)__shfl((int)depth, src) - 1u;
                     if (want_off && ks < n) {  // offloaded: go on with the scattered ray
-                        light[(depth - 1) * BLOCK] = -light[(depth - 1) * BLOCK];
+                        light[(depth - 1) * LS] = -light[(depth - 1) * LS];
                         sany = false;
                         if (depth < (uint32_t)kMaxDepth) {
-                            sd = mk(nxt[3 * BLOCK], nxt[4 * BLOCK], nxt[5 * BLOCK]);
+                            sd = mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
                         } else {
                             start = false;
                             finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
@@ -1009,12 +1015,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             if (finish) {
                 bool pend = false;
                 if (HELP)
-                    for (int kk = 0; kk < (int)depth; ++kk) pend |= light[kk * BLOCK] < 0.0f;
+                    for (int kk = 0; kk < (int)depth; ++kk) pend |= light[kk * LS] < 0.0f;
                 waiting = pend;
                 if (!pend) {
                     if (SAMP != 3)
                         for (int kk = (int)depth - 1; kk >= 0; --kk)
-                            color = backward_step(color, light[kk * BLOCK]);
+                            color = backward_step(color, light[kk * LS]);
                     if (SAMP == 2 && pc.sbuf) {  // a chain sample traced in full: k_resolve sums in order
                         typedef float f32x4 __attribute__((ext_vector_type(4)));
                         __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
@@ -1944,6 +1950,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         constexpr int kSparseS = kSparse;
         fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>
                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>;
+        // TMPT_SAMPLE_OCC=5 (A/B): 5 waves per SIMD, light terms and the pending
+        // ray in global memory (k_path kGL)
+        if (const char* e = getenv("TMPT_SAMPLE_OCC"))
+            if (atoi(e) == 5 && !count) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 5, kSparseS, 0, 0, 1>;
         if (prof)  // TMPT_PROF=1|2 (diagnostic): wave-time split of the sample kernel
             fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 2, 0, 1>
                                : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 1, 0, 1>;
@@ -2044,7 +2054,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
     const size_t reg_words = ordered ? 2 * (size_t)kSimdKeys + 64 + (size_t)P : 0;  // + claim words
     const size_t extra_words = ordered ? (size_t)P * (4 + 5) + hist_words + reg_words : 0;
-    if (ensure_ws(s, (ovf_words + head_words + extra_words) * 4)) return -1;
+    const bool gl = fn == (PathFn)k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 5, kSparse, 0, 0, 1>;
+    const size_t gl_words = gl ? (size_t)grid * kBlk * (kMaxDepth + 6) : 0;
+    if (ensure_ws(s, (ovf_words + head_words + extra_words + gl_words) * 4)) return -1;
     uint32_t* heads = (uint32_t*)s.ws + ovf_words;
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
     PathCtl pc;
@@ -2068,6 +2080,12 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.nblk = nblk;
     pc.blk = blk;
     pc.sbuf = nullptr;
+    pc.upix = pc.ustate = pc.uslot = nullptr;
+    pc.rs_out = nullptr;
+    pc.rs_end = nullptr;
+    pc.p_dev = nullptr;
+    pc.rs_noshadow = 0;
+    pc.gl_store = gl ? reinterpret_cast<float*>((uint32_t*)s.ws + ovf_words + head_words + extra_words) : nullptr;
     RenderArgs as = a;  // sample seeding: a lane's run of samples is its block
     if (a.jt) {
         as.bmask = nblk > 1 ? blk - 1u : 2047u;
