@@ -60,6 +60,20 @@ S_NODE = 64            # bytes per visited node: BVH4Q (4 quantised child boxes 
 S_TRI = 36             # bytes per triangle test (3 x vec3), SURVEY.md §8d
 S_RAY = 32 + 16        # ray read + hit write, SURVEY.md §8d
 
+# What each seeding mode is (tmpt.h TMPT_SEED_*).  Only row
+# seeding threads the reference's own stream (main.cpp:204) and so reproduces
+# the reference binary's image; pixel and sample seeding are the north star's
+# "same per-pixel xorshift seed" contract, each byte-exact against its oracle leg.
+RNG_CONTRACT = {
+    "sample": "per-pixel seed (y*W+x)*9781+1; sample s starts 2^16*s xorshift steps into the pixel's stream "
+              "(NOT the reference's row-chained stream: statistically equivalent image, not the reference "
+              "binary's bytes; reference-exact row seeding is timed under seed_modes.row)",
+    "pixel": "per-pixel seed (y*W+x)*9781+1, the pixel's samples in sequence (NOT the reference's row-chained "
+             "stream; reference-exact row seeding is timed under seed_modes.row)",
+    "row": "the reference's own seeding, unmodified: y*9781+1 per row, threaded through the row's pixels and "
+           "samples (main.cpp:204); byte-identical to the reference binary",
+}
+
 CONFIGS = {
     # name: (obj, width, height, spp, is_sponza)
     "sponza1080": ("sponza", 1920, 1080, 64, True),    # BASELINE configs[3]: the metric's config
@@ -96,6 +110,74 @@ def pmc_traffic() -> dict:
             "traffic_source": os.path.relpath(files[-1], ROOT), "traffic_kernel": rec["kernel"]}
 
 
+def host_cpus() -> dict:
+    """Host cores as the reference's TBB would see them (main.cpp:250-251:
+    task_scheduler_init(default_num_threads()) = every core the process may
+    run on) and the cgroup CPU quota the box enforces, if any."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"nproc": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota, "cpu_model": model}
+
+
+def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
+    """The CPU restatement of the reference algorithm (octree + Moller-Trumbore,
+    oracle/) on ALL host cores -- as many threads as the process may use, like
+    TBB's default_num_threads() (main.cpp:250-251) -- timed on a bounded sample
+    of the same frame: batches of rows y = o (mod S), S ~ H / (2 threads) (two rows per
+    thread), of which the pixels x = c (mod 16) (pixel and sample seeding:
+    pixels are independent; row seeding renders whole rows of fewer rows per
+    batch, its stream runs along the row), batches in a fixed scattered order
+    until ~args.cpu_seconds have passed.  Also compares those pixels with the
+    GPU frame (octree tie order)."""
+    import oracle
+    hc = host_cpus()
+    threads = max(1, min(hc["nproc"], 256))  # the oracle's thread pool holds at most 256
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
+    seed = {"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL, "row": oracle.SEED_ROW}[args.seed_mode]
+    row_mode = args.seed_mode == "row"
+    xs = 1 if row_mode else 16
+    stride = max(1, H // (16 if row_mode else 2 * threads))
+    batches = [(o, c) for c in range(xs) for o in range(stride)]
+    order = [batches[(k * 7919) % len(batches)] for k in range(len(batches))] \
+        if len(batches) % 7919 else batches
+    ref = np.zeros((H, W, 4), np.uint8)
+    mask = np.zeros((H, W), bool)
+    crays, cdt, nb = 0, 0.0, 0
+    for o, c in order:
+        t1 = time.perf_counter()
+        _, r = osc.render(cam.as_array(), W, H, SPP, seed_mode=seed, y0=o, row_step=stride, x0=c, x_step=xs,
+                          threads=threads, rgba=ref)
+        cdt += time.perf_counter() - t1
+        crays += r
+        mask[o::stride, c::xs] = True
+        nb += 1
+        if cdt >= args.cpu_seconds:
+            break
+    npx = int(mask.sum())
+    cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads, "kind": "port",
+           "threads": threads, **hc,
+           "sample": f"{npx} of {W * H} px ({nb} batches of rows y%{stride}==o, pixels x%{xs}==c) x {SPP} spp, "
+                     f"{crays} rays, {cdt:.1f} s on {threads} threads (the box grants "
+                     f"{hc['cgroup_cpu_quota'] or hc['nproc']} CPUs); octree restatement of scene.cpp, "
+                     f"{args.seed_mode} seeding"}
+    diff = int(((frame != ref).any(-1) & mask).sum())
+    parity = {"pixels_checked": npx, "pixels_differ": diff, "oracle": "octree (reference tie order)"}
+    return cpu, parity
+
+
 @contextlib.contextmanager
 def stdout_to_stderr():
     """Point file descriptor 1 at stderr for the duration (native libraries
@@ -119,12 +201,15 @@ def main() -> None:
     ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
     ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
     ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel", "row"])
-    ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding mode")
+    ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding modes")
+    ap.add_argument("--compare", action="store_true",
+                    help="time the other seeding modes at N>1 too (default: only at N=1, so the driver's "
+                         "multi-GPU runs are not slowed)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the collective path (process group, gather, max-over-ranks) even at one rank "
                          "(tests the RCCL calls on a 1-GPU box)")
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
-    ap.add_argument("--cpu-row-step", type=int, default=64, help="CPU baseline: every k-th row")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline: time budget of the row sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--save", default="", help="rank 0 writes the frame as PNG here")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -224,7 +309,7 @@ def main() -> None:
     # ---- the other seeding mode, timed the same way (reported, not `value`)
     frame = image.cpu().numpy() if rank == 0 else None
     compare = {}
-    if not args.no_compare:
+    if not args.no_compare and (world == 1 or args.compare):
         for name, sd in seeds.items():
             if sd == seed:
                 continue
@@ -305,29 +390,7 @@ def main() -> None:
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu:
-        import oracle
-        threads = min(16, os.cpu_count() or 1)
-        osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
-        t1 = time.perf_counter()
-        ref, crays = osc.render(cam.as_array(), W, H, SPP,
-                                seed_mode={"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL,
-                                           "row": oracle.SEED_ROW}[args.seed_mode],
-                                row_step=args.cpu_row_step, threads=threads)
-        cdt = time.perf_counter() - t1
-        rows = np.arange(0, H, args.cpu_row_step)
-        cpu_model = ""
-        try:
-            with open("/proc/cpuinfo") as f:
-                cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
-        except OSError:
-            pass
-        cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads,
-               "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model,
-               "sample": f"rows y%{args.cpu_row_step}==0 ({len(rows)} x {W} px x {SPP} spp, "
-                         f"{crays} rays, {cdt:.1f} s), octree restatement of scene.cpp, {args.seed_mode} seeding"}
-        diff = int((frame[rows] != ref[rows]).any(-1).sum())
-        parity = {"rows_checked": int(len(rows)), "pixels_differ": diff,
-                  "oracle": "octree (reference tie order)"}
+        cpu, parity = cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame)
 
     if args.save:
         tm.write_png(args.save, frame)
@@ -370,7 +433,8 @@ def main() -> None:
                 "floor, data/gen_standin_sponza.py)" if sponza else "data/*.obj from the reference",
         "config": {"workload": f"{args.config}: {os.path.basename(path)} {W}x{H} {SPP}spp",
                    "global_batch": W * H, "spp": SPP, "tris": int(tris.shape[0]),
-                   "seed_mode": args.seed_mode, "engine": args.engine,
+                   "seed_mode": args.seed_mode, "rng": RNG_CONTRACT[args.seed_mode],
+                   "image_is_reference_binary_image": args.seed_mode == "row", "engine": args.engine,
                    "parallelism": f"row-bands{BAND_ROWS}x{world}",
                    "rays_per_step": rays // args.steps},
         "seed_modes": compare,

@@ -22,10 +22,13 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 5  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+#define TMPT_ABI_VERSION 6  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
                               4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
                               progressive continuation keyed on the camera,
-                              TMPT_SEED_SAMPLE */
+                              TMPT_SEED_SAMPLE; 6: scene options (tmpt_scene_create_ex,
+                              tmpt_scene_set_option / get_option) replace the
+                              library's environment variables, tmpt_scene_hit_ranged
+                              (per-ray tmin / tmax), tmpt_render_multi gathers over RCCL */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -58,7 +61,8 @@ enum {
 enum {
     TMPT_FLAG_OUT_DEVICE = 1,    /* rgba_out is a device pointer on the scene's device */
     TMPT_FLAG_COUNT_VISITS = 2,  /* instrumented traversal: node visits / triangle tests */
-    TMPT_FLAG_WAIT_STREAM = 4    /* the render starts after the work enqueued on desc->wait_stream */
+    TMPT_FLAG_WAIT_STREAM = 4,   /* the render starts after the work enqueued on desc->wait_stream */
+    TMPT_FLAG_REQUIRE_RCCL = 8   /* tmpt_render_multi: fail unless the gather runs over RCCL */
 };
 
 /* One render call = one shard of one frame (TraceImageBody over its rows,
@@ -134,8 +138,43 @@ int tmpt_device_count(void);
 
 /* Scene::Scene (scene.h:19, scene.cpp:97-100) + Scene::BuildOctree
  * (scene.h:26, scene.cpp:118-126): copies n triangles (n*9 floats, v0 v1 v2)
- * to `device` and builds the LBVH there.  The caller keeps ownership of tris. */
+ * to `device` and builds the BVH there.  The caller keeps ownership of tris.
+ * tmpt_scene_create = tmpt_scene_create_ex with no options. */
 int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene** out);
+
+/* Scene options: the library's whole control plane (no environment variables;
+ * the reference has no counterpart -- its constants are compiled in).  Every
+ * option has a default that reproduces the measured-best configuration; all of
+ * them change speed, never the image or the HitScene answers.
+ * `options` = "key=value,key=value" (NULL or "" = defaults); an unknown key or
+ * a value out of range is an error (-22).
+ * Build options (only at creation):
+ *   builder      ploc (0, default) | lbvh (1): PLOC (Meister & Bittner 2018) or
+ *                Karras 2012 LBVH over the same 30-bit Morton order
+ *   leaf_max     triangles per BVH4 leaf, 1..16 (default 2)
+ *   collapse     greedy (0, default) | sah (1): BVH2 -> BVH4 collapse
+ *   ploc_radius  PLOC search radius, 1..256 (default 32)
+ *   sah_c_leaf, sah_c_tri  SAH collapse costs (defaults 0.7, 0.5; inner node 1)
+ * Render options (tmpt_scene_set_option; apply to later renders on the scene):
+ *   sample_block     sample seeding: samples per work unit, power of two (0 = auto)
+ *   sbuf_max         sample seeding: cap in bytes on the per-sample colour
+ *                    buffer (0 = 3/4 of free HBM); over the cap a pixel is one unit
+ *   pilot            pixel seeding: pilot samples of the cost-ordered supply (-1 = auto, 0 = off)
+ *   help, pair       pixel seeding: shadow offload to idle lanes (-1 = auto, 0, 1)
+ *                    and expensive ranks per 64-rank chunk (-1 = auto, 0..63)
+ *   balance, dprio   pixel seeding: SIMD-balanced first chunks (1), longest-
+ *                    remaining-first wave priority with offload (1)
+ *   wave_cap         pixel seeding: pixels a wave holds at once (0 = auto, 1..64)
+ *   rowspec          row seeding on the persistent engine: 1 = speculative row
+ *                    engine, 0 = one lane per row chain
+ *   rowspec_wmax, rowspec_windows, rowspec_spread, rowspec_groups,
+ *   rowspec_noshadow speculative row engine: units per window (0 = auto),
+ *                    windows per row and iteration (0 = auto, 1..32), window
+ *                    spread in pixels (-1 = auto), row groups/streams (1..8),
+ *                    shadow-free speculation + one full re-trace (1) */
+int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);
+int tmpt_scene_set_option(tmpt_scene* scene, const char* key, double value);
+int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* value);
 /* Scene::~Scene (scene.h:20) */
 int tmpt_scene_destroy(tmpt_scene* scene);
 
@@ -147,6 +186,11 @@ int tmpt_scene_destroy(tmpt_scene* scene);
  * ids[i] >= 0 is meaningful).  Host pointers. */
 int tmpt_scene_hit(const tmpt_scene* scene, const float* rays, int64_t n, float tmin, float tmax,
                    int32_t any_hit, float* hits, int32_t* ids);
+/* The same with the range per ray, as each HitScene call takes it
+ * (scene.h:36-37: HitScene(ray, tMin, tMax, hit)): rays8 = n x {orig.xyz,
+ * dir.xyz, tmin, tmax}.  t is accepted in [tmin, tmax]. */
+int tmpt_scene_hit_ranged(const tmpt_scene* scene, const float* rays8, int64_t n, int32_t any_hit,
+                          float* hits, int32_t* ids);
 
 /* tbb::parallel_for(rows, TraceImageBody) (main.cpp:329-331, 180-246):
  * renders desc's shard into rgba_out (tmpt_tile_rows(desc) * width * 4 bytes).
@@ -155,12 +199,18 @@ int tmpt_render(tmpt_scene* scene, const tmpt_camera* cam, const tmpt_render_des
                 uint8_t* rgba_out, uint64_t* ray_count);
 /* main.cpp:312-331 over several devices in ONE process (SURVEY.md §8e's
  * single-process form): a scene per entry of devices[] (created here, freed on
- * return; a device may repeat), the frame's rows dealt round-robin to
- * them, one host thread per device, the tiles assembled into rgba_full
- * (width*height*4, row 0 = bottom, as tmpt_render).  desc's band_rows, shard,
- * num_shards and flags are taken over; *seconds = wall time of the renders
- * (scene builds excluded, main.cpp:319-333); *ray_count = all devices' rays.
- * The one-process-per-GPU form is bench.py (torch.distributed + RCCL). */
+ * return), the frame's rows dealt round-robin to them (1-row bands), one host
+ * thread per device rendering into a device tile, then ONE RCCL gather
+ * (ncclCommInitAll over devices[], ncclGather of the equal-size tiles to
+ * devices[0] over xGMI, ncclReduce of the uint64 ray counts) and the rows
+ * de-interleaved on devices[0] into rgba_full (width*height*4, row 0 =
+ * bottom, as tmpt_render).  RCCL ranks need distinct devices: with a device
+ * listed twice the gather is device-to-device copies instead (or an error
+ * with TMPT_FLAG_REQUIRE_RCCL in desc->flags).  desc's band_rows, shard and
+ * num_shards are taken over; *seconds = wall time from the renders' start to
+ * the assembled frame on devices[0] (scene builds excluded, main.cpp:319-333);
+ * *ray_count = all devices' rays.  The one-process-per-GPU form is bench.py
+ * (torch.distributed + RCCL). */
 int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, const tmpt_render_desc* desc,
                       const int32_t* devices, int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count,
                       double* seconds);

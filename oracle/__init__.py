@@ -77,6 +77,11 @@ _render = _sig("orc_render", ctypes.c_uint64, [ctypes.c_void_p, ctypes.POINTER(_
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_void_p])
+_render_ex = _sig("orc_render_ex", ctypes.c_uint64, [ctypes.c_void_p, ctypes.POINTER(_Camera), ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_void_p])
 _trace = _sig("orc_trace", None, [ctypes.c_void_p, _f32p, _f32p, _u32p, _f32p,
                                   ctypes.POINTER(ctypes.c_uint64)])
 _sincos = _sig("orc_unit_angle_sincos", None, [ctypes.c_uint32, _f32p, _f32p])
@@ -228,13 +233,17 @@ class Scene:
         return list(a)
 
     def render(self, cam_arr, w, h, spp, seed_mode=SEED_ROW, y0=0, y1=None, row_step=1,
-               threads=None, rgba=None):
-        """Rows y0, y0+row_step, ... < y1 into a full-frame rgba (H, W, 4), row 0 = bottom."""
+               threads=None, rgba=None, x0=0, x_step=1):
+        """Rows y0, y0+row_step, ... < y1 into a full-frame rgba (H, W, 4), row 0 = bottom;
+        of each row the pixels x0, x0+x_step, ... (pixel / sample seeding; row
+        seeding always renders whole rows).  threads: default every CPU this
+        process may run on."""
         if rgba is None:
             rgba = np.zeros((h, w, 4), np.uint8)
-        threads = threads or os.cpu_count() or 1
-        rays = _render(self._h, ctypes.byref(_cam_from_arr(cam_arr)), w, h, spp, seed_mode, y0,
-                       h if y1 is None else y1, row_step, threads, rgba.ctypes.data_as(ctypes.c_void_p))
+        threads = threads or len(os.sched_getaffinity(0)) or 1
+        rays = _render_ex(self._h, ctypes.byref(_cam_from_arr(cam_arr)), w, h, spp, seed_mode, y0,
+                          h if y1 is None else y1, row_step, x0, x_step, threads,
+                          rgba.ctypes.data_as(ctypes.c_void_p))
         return rgba, int(rays)
 
     def trace(self, orig, direction, seed):

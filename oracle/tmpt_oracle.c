@@ -823,16 +823,23 @@ void orc_trace(const orc_scene* s, const float orig[3], const float dir[3], uint
  * row (main.cpp:204, the stream threads along the row), pixel (one stream per
  * pixel, its samples in sequence) or sample (sample smp of the pixel starts at
  * M^(smp * 2^16) of the pixel seed: jumps[smp] = that matrix's columns). */
+/* Pixels x = xa, xa + xs, ... < xb of row y (row seeding: always the whole
+ * row, its stream runs through every pixel). */
 static uint64_t render_row(const orc_scene* s, const orc_camera* cam, int32_t w, int32_t h,
-                           int32_t spp, int32_t seed_mode, int64_t y, uint8_t* image,
-                           const uint32_t* jumps)
+                           int32_t spp, int32_t seed_mode, int64_t y, int64_t xa, int64_t xb, int64_t xs,
+                           uint8_t* image, const uint32_t* jumps)
 {
     const float invWidth = 1.0f / (float)w;     /* main.cpp:186 */
     const float invHeight = 1.0f / (float)h;    /* main.cpp:187 */
     const float sppRecip = 1.0f / (float)spp;   /* main.cpp:188 */
     uint64_t rays = 0;
     uint32_t rngState = (uint32_t)y * 9781u + 1u; /* main.cpp:204 */
-    for (int64_t x = 0; x < w; ++x) {
+    if (seed_mode == ORC_SEED_ROW) {
+        xa = 0;
+        xb = w;
+        xs = 1;
+    }
+    for (int64_t x = xa; x < xb; x += xs) {
         if (seed_mode == ORC_SEED_PIXEL) rngState = orc_pixel_seed((int32_t)x, (int32_t)y, w);
         v3 col = V(0.0f, 0.0f, 0.0f);
         const uint32_t pseed = orc_pixel_seed((int32_t)x, (int32_t)y, w);
@@ -858,13 +865,19 @@ static uint64_t render_row(const orc_scene* s, const orc_camera* cam, int32_t w,
     return rays;
 }
 
+/* Work units: rows (grain 1, main.cpp:329-331), or -- pixel and sample
+ * seeding, where pixels are independent -- row pieces of kUnitPixels
+ * rendered pixels, so a few rows still spread over every thread. */
+enum { kUnitPixels = 64 };
+
 typedef struct {
     const orc_scene* s;
     const orc_camera* cam;
-    int32_t w, h, spp, seed_mode, y0, y1, step;
+    int32_t w, h, spp, seed_mode, y0, y1, step, x0, xstep;
+    int64_t pieces; /* units per row */
     uint8_t* rgba;
     const uint32_t* jumps;
-    atomic_int next;
+    atomic_llong next;
     atomic_ullong rays;
 } render_job;
 
@@ -873,10 +886,16 @@ static void* render_worker(void* arg)
     render_job* j = (render_job*)arg;
     uint64_t local = 0;
     for (;;) {
-        int k = atomic_fetch_add(&j->next, 1); /* grain size 1, main.cpp:329-331 */
-        int64_t y = (int64_t)j->y0 + (int64_t)k * j->step;
+        int64_t k = atomic_fetch_add(&j->next, 1);
+        int64_t r = k / j->pieces, p = k - r * j->pieces;
+        int64_t y = (int64_t)j->y0 + r * j->step;
         if (y >= j->y1) break;
-        local += render_row(j->s, j->cam, j->w, j->h, j->spp, j->seed_mode, y, j->rgba, j->jumps);
+        const int64_t span = (int64_t)kUnitPixels * j->xstep;
+        const int64_t xa = j->x0 + p * span;
+        int64_t xb = xa + span;
+        if (xb > j->w) xb = j->w;
+        local += render_row(j->s, j->cam, j->w, j->h, j->spp, j->seed_mode, y, xa, xb, j->xstep, j->rgba,
+                            j->jumps);
     }
     atomic_fetch_add(&j->rays, local);
     return NULL;
@@ -886,13 +905,31 @@ uint64_t orc_render(const orc_scene* s, const orc_camera* cam, int32_t w, int32_
                     int32_t seed_mode, int32_t y0, int32_t y1, int32_t row_step, int32_t nthreads,
                     uint8_t* rgba)
 {
+    return orc_render_ex(s, cam, w, h, spp, seed_mode, y0, y1, row_step, 0, 1, nthreads, rgba);
+}
+
+uint64_t orc_render_ex(const orc_scene* s, const orc_camera* cam, int32_t w, int32_t h, int32_t spp,
+                       int32_t seed_mode, int32_t y0, int32_t y1, int32_t row_step, int32_t x0,
+                       int32_t x_step, int32_t nthreads, uint8_t* rgba)
+{
     render_job j;
     j.s = s; j.cam = cam; j.w = w; j.h = h; j.spp = spp; j.seed_mode = seed_mode;
     j.y0 = y0; j.y1 = y1 < h ? y1 : h; j.step = row_step > 0 ? row_step : 1; j.rgba = rgba;
+    j.x0 = x0 < 0 ? 0 : x0;
+    j.xstep = x_step > 0 ? x_step : 1;
+    if (seed_mode == ORC_SEED_ROW) {
+        j.x0 = 0;
+        j.xstep = 1;
+        j.pieces = 1;
+    } else {
+        const int64_t npx = j.x0 < w ? (w - j.x0 + j.xstep - 1) / j.xstep : 0;
+        j.pieces = npx > 0 ? (npx + kUnitPixels - 1) / kUnitPixels : 1;
+    }
     uint32_t* jumps = NULL;
     if (seed_mode == ORC_SEED_SAMPLE) { /* M^(smp * stride) for every sample index */
         uint32_t stride[32];
         jumps = (uint32_t*)malloc(sizeof(uint32_t) * 32 * (size_t)(spp > 0 ? spp : 1));
+        if (!jumps) return 0;
         orc_jump_matrix(ORC_SAMPLE_STRIDE, stride);
         for (int b = 0; b < 32; ++b) jumps[b] = 1u << b;
         for (int32_t k = 1; k < spp; ++k) orc_gf2_mul(stride, jumps + 32 * (k - 1), jumps + 32 * k);

@@ -94,6 +94,12 @@ void       orc_scene_stats(const orc_scene* s, int64_t out[4]);
 uint64_t orc_render(const orc_scene* s, const orc_camera* cam, int32_t w, int32_t h,
                     int32_t spp, int32_t seed_mode, int32_t y0, int32_t y1,
                     int32_t row_step, int32_t nthreads, uint8_t* rgba);
+/* The same over the pixels x = x0, x0 + x_step, ... of each of those rows
+ * (pixel and sample seeding; row seeding renders whole rows: its stream runs
+ * through every pixel of the row).  Returns 0 rays if out of memory. */
+uint64_t orc_render_ex(const orc_scene* s, const orc_camera* cam, int32_t w, int32_t h,
+                       int32_t spp, int32_t seed_mode, int32_t y0, int32_t y1,
+                       int32_t row_step, int32_t x0, int32_t x_step, int32_t nthreads, uint8_t* rgba);
 
 /* One path (Trace, main.cpp:82-119) from a given ray; rng advanced in place.
  * Returns the colour; *rays incremented by the HitScene calls made. */

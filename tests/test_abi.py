@@ -42,7 +42,7 @@ def test_no_oracle_or_torch_in_the_product_library():
 
 
 def test_abi_version_and_error_channel():
-    assert tm.abi_version() == 5
+    assert tm.abi_version() == 6
     with pytest.raises(tm.TmptError) as e:
         tm.load_scene("/definitely/missing.obj")
     assert "missing.obj" in str(e.value)
@@ -82,3 +82,35 @@ def test_cli_usage_without_gpu():
     assert r.returncode == 1 and "invalid width" in r.stdout
     r = subprocess.run([cli, "10", "10", "2000", "x.obj"], capture_output=True, text=True)
     assert r.returncode == 1 and "invalid samplesPerPixel" in r.stdout
+
+
+def test_product_library_reads_no_environment_knobs():
+    """The library's control plane is the per-scene options API (tmpt.h "Scene
+    options"); in the product build only the host's OBJ / PNG thread counts
+    come from the environment (the diagnostic TMPT_DIAG build adds traces)."""
+    csrc = os.path.join(ROOT, "toymeshpathtracer_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            text = open(os.path.join(csrc, f)).read()
+            text = re.sub(r"#ifdef TMPT_DIAG.*?#endif", "", text, flags=re.S)
+            names |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', text))
+            names |= set(re.findall(r'(?:env_int|host_threads)\("([A-Z_0-9]+)"', text))
+    assert names <= {"TMPT_OBJ_THREADS", "TMPT_PNG_THREADS", "TMPT_OBJ_CHUNK", "TMPT_PNG_STRIP"}, names
+
+
+def test_scene_options_are_checked_before_any_device_work():
+    """tmpt_scene_create_ex parses its options first: an unknown key, a bad
+    value or a value out of range is -22 with a message; valid options get as
+    far as the device lookup (no GPU here)."""
+    import numpy as np
+    tris = np.zeros((1, 9), np.float32)
+    for bad, msg in (("bogus=1", "unknown option"), ("leaf_max=0", "out of range"), ("leaf_max=x", "bad value"),
+                     ("builder=kd", "bad value"), ("sample_block=3", "power of two"), ("leaf_max", "no value"),
+                     ("pilot=1.5", "integer")):
+        with pytest.raises(tm.TmptError, match=msg):
+            tm.Scene(tris, options=bad)
+    if tm.device_count() == 0:
+        for good in ("builder=lbvh, leaf_max=4", {"collapse": "sah", "ploc_radius": 8}, "", None):
+            with pytest.raises(tm.TmptError, match="device"):
+                tm.Scene(tris, options=good)

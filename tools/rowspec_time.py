@@ -2,10 +2,12 @@
 the speculative row engine's variants against each other, interleaved in one
 process; every variant's image and ray count must equal the first one's.
 
-  python tools/rowspec_time.py "TMPT_ROWSPEC_GROUPS=1;TMPT_ROWSPEC_GROUPS=2&TMPT_ROWSPEC_MARGIN=1.3" [spp] [rounds]
+  python tools/rowspec_time.py "rowspec_groups=1;rowspec_groups=2&rowspec_windows=4" [spp] [rounds]
 
-ENGINE=mega in a variant runs the one-lane-per-row megakernel instead.
-TMPT_ROWSPEC_LOG=1 prints iterations and the speculation factor per render."""
+Variants are scene render options (include/tmpt.h); ENGINE=mega runs the
+one-lane-per-row megakernel instead.  With the diagnostic library build
+(make DIAG=1, TMPT_LIB_PATH) TMPT_ROWSPEC_LOG=1 prints iterations and the
+speculation factor per render."""
 import os
 import sys
 import time
@@ -18,7 +20,6 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-KEYS = ("TMPT_ROWSPEC_GROUPS", "TMPT_ROWSPEC_MARGIN", "TMPT_ROWSPEC_WMAX", "TMPT_ROWSPEC", "TMPT_ROWSPEC_GDIV", "TMPT_ROWSPEC_CHUNK", "TMPT_ROWSPEC_LOOK", "TMPT_ROWSPEC_LO", "TMPT_ROWSPEC_SPREAD", "TMPT_ROWSPEC_NOSHADOW", "TMPT_ROWSPEC_OCC")
 
 
 def main():
@@ -30,16 +31,18 @@ def main():
     tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
     sc = tm.Scene(tris)
+    defaults = {k: sc.get_option(k) for k in ("rowspec", "rowspec_wmax", "rowspec_windows", "rowspec_spread",
+                                              "rowspec_groups", "rowspec_noshadow")}
     ref = None
     res = {v: [] for v in variants}
     for _ in range(rounds):
         for v in variants:
             env = dict(kv.split("=", 1) for kv in v.split("&") if kv)
-            for k in KEYS:
-                os.environ.pop(k, None)
+            for k, val in defaults.items():
+                sc.set_option(k, val)
             for k, val in env.items():
                 if k != "ENGINE":
-                    os.environ[k] = val
+                    sc.set_option(k, float(val))
             eng = tm.ENGINE_MEGAKERNEL if env.get("ENGINE") == "mega" else tm.ENGINE_PERSISTENT
             t0 = time.perf_counter()
             img, rays = sc.trace_image(cam, W, H, spp, seed_mode=tm.SEED_ROW, engine=eng, band_rows=1,

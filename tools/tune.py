@@ -1,13 +1,15 @@
-"""Interleaved A/B of build/traversal variants in ONE process on the bench frame
-(sponza stand-in 1920x1080, pixel seeding; MI355X_MICROARCH-style rule: compare
-variants in one process, interleaved rounds).
+"""Interleaved A/B of scene-option variants in ONE process on the bench frame
+(sponza stand-in 1920x1080, pixel seeding by default; MI355X_MICROARCH-style
+rule: compare variants in one process, interleaved rounds).
 
-  python tools/tune.py "TMPT_BUILDER=lbvh;TMPT_BUILDER=ploc&TMPT_PLOC_R=16;TMPT_TUNE=16,4,16,1" [spp] [rounds]
+  python tools/tune.py "builder=lbvh;ploc_radius=16&leaf_max=4;sample_block=2&ENGINE=wavefront" [spp] [rounds]
 
-Variants are separated by ';', env assignments within a variant by '&'.  Build-time keys
-(TMPT_BUILDER, TMPT_LEAF_MAX, TMPT_PLOC_R) select a scene built once per
-distinct setting; render-time keys (TMPT_TUNE, TMPT_BVH) are set per render.
-Every variant's image must equal the first one's (bit-exact contract)."""
+Variants are separated by ';', options within a variant by '&' (include/tmpt.h
+"Scene options").  Build options select a scene built once per distinct
+setting; render options are set on it before each render; ENGINE picks the
+engine.  Every variant's image must equal the first one's (bit-exact contract).
+Harness settings: TUNE_SCENE, TUNE_SHARDS, TUNE_BAND, TUNE_SEED, TUNE_RES,
+TUNE_COUNT; another library build: TMPT_LIB_PATH (one per process)."""
 import os
 import sys
 import time
@@ -20,8 +22,7 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-BUILD_KEYS = ("TMPT_TREELET", "TMPT_TREELET_MIN", "TMPT_LAYOUT", "TMPT_BUILDER", "TMPT_LEAF_MAX", "TMPT_PLOC_R", "TMPT_COLLAPSE", "TMPT_SAH_CLEAF", "TMPT_SAH_CTRI")
-RENDER_KEYS = ("TMPT_SAMPLE_OCC", "TMPT_SAMPLE_BLOCK", "TMPT_SBUF", "TMPT_TUNE", "TMPT_BVH", "TMPT_NODE", "TMPT_PROF", "TMPT_PILOT", "TMPT_PILOT_RATIO", "TMPT_SHADOW_GRID", "TMPT_PRIO", "TMPT_WAVE_CAP", "TMPT_HELP", "TMPT_PAIR", "TMPT_BALANCE", "TMPT_BLOCKS_PER_CU", "TMPT_DPRIO", "TMPT_BALANCE_LOG", "TMPT_DIAG_NOSHADOW")
+BUILD_KEYS = ("builder", "leaf_max", "collapse", "ploc_radius", "sah_c_leaf", "sah_c_tri")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
@@ -46,16 +47,16 @@ def parse(v):
 
 
 scenes = {}
+with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after each variant
+    DEFAULTS = {k: _probe.get_option(k) for k in ("sample_block", "sbuf_max", "pilot", "help", "pair", "balance", "dprio",
+                                                  "wave_cap", "rowspec", "rowspec_wmax", "rowspec_windows",
+                                                  "rowspec_spread", "rowspec_groups", "rowspec_noshadow")}
 
 
 def scene_for(env):
     key = tuple((k, env.get(k)) for k in BUILD_KEYS)
     if key not in scenes:
-        for k in BUILD_KEYS:
-            os.environ.pop(k, None)
-            if env.get(k) is not None:
-                os.environ[k] = env[k]
-        sc = tm.Scene(tris)
+        sc = tm.Scene(tris, options={k: v for k, v in key if v is not None})
         st = sc.stats()
         print(f"scene {dict(key)}: build {st.build_ms:.1f} ms, bvh4 nodes {st.bvh4_nodes}, depth4 "
               f"{st.bvh4_depth}, ploc iters {st.builder_iters}", flush=True)
@@ -74,18 +75,20 @@ for r in range(rounds):
     for v in variants:
         env = parse(v)
         sc = scene_for(env)
-        for k in RENDER_KEYS:
-            os.environ.pop(k, None)
-            if env.get(k) is not None:
-                os.environ[k] = env[k]
+        for k, val in env.items():  # render options: set for this render, defaults otherwise
+            if k not in BUILD_KEYS and k != "ENGINE":
+                sc.set_option(k, float(val))
         t0 = time.perf_counter()
         img, rays = sc.trace_image(cam, W, H, spp, seed_mode=SEED, band_rows=BAND, shard=0,
                                    num_shards=SHARDS, engine=ENGINES[env.get("ENGINE", "persistent")])
         dt = time.perf_counter() - t0
         st = sc.stats()
+        for k in env:
+            if k not in BUILD_KEYS and k != "ENGINE":
+                sc.set_option(k, DEFAULTS[k])
         if ref is None:
             ref, ref_rays = img, rays
-        assert "TMPT_DIAG" in v or np.array_equal(img, ref), f"variant {v!r} changed the image"
+        assert np.array_equal(img, ref), f"variant {v!r} changed the image"
         assert rays == ref_rays, f"variant {v!r} changed the ray count ({rays} vs {ref_rays})"
         res[v].append((rays / dt / 1e6, st.extend_ms, st.shadow_ms, dt * 1e3))
 for v, xs in res.items():

@@ -34,7 +34,7 @@ __all__ = [
 
 SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
 ENGINE_WAVEFRONT, ENGINE_MEGAKERNEL, ENGINE_PERSISTENT = 0, 1, 2
-FLAG_OUT_DEVICE, FLAG_COUNT_VISITS, FLAG_WAIT_STREAM = 1, 2, 4
+FLAG_OUT_DEVICE, FLAG_COUNT_VISITS, FLAG_WAIT_STREAM, FLAG_REQUIRE_RCCL = 1, 2, 4, 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMPT_LIB_PATH: another in-tree build of the library (compiler-flag A/B in tools/)
@@ -116,10 +116,17 @@ _cam_scene = _sig("tmpt_camera_for_scene", ctypes.c_int, [ctypes.POINTER(_Camera
 _dev_count = _sig("tmpt_device_count", ctypes.c_int, [])
 _scene_create = _sig("tmpt_scene_create", ctypes.c_int, [_f32p, ctypes.c_int32, ctypes.c_int32,
                                                          ctypes.POINTER(ctypes.c_void_p)])
+_scene_create_ex = _sig("tmpt_scene_create_ex", ctypes.c_int, [_f32p, ctypes.c_int32, ctypes.c_int32,
+                                                               ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)])
+_set_option = _sig("tmpt_scene_set_option", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_double])
+_get_option = _sig("tmpt_scene_get_option", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
+                                                           ctypes.POINTER(ctypes.c_double)])
 _scene_destroy = _sig("tmpt_scene_destroy", ctypes.c_int, [ctypes.c_void_p])
 _scene_hit = _sig("tmpt_scene_hit", ctypes.c_int, [ctypes.c_void_p, _f32p, ctypes.c_int64,
                                                    ctypes.c_float, ctypes.c_float, ctypes.c_int32,
                                                    _f32p, _i32p])
+_scene_hit_ranged = _sig("tmpt_scene_hit_ranged", ctypes.c_int, [ctypes.c_void_p, _f32p, ctypes.c_int64,
+                                                                 ctypes.c_int32, _f32p, _i32p])
 _render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Camera),
                                              ctypes.POINTER(_Desc), ctypes.c_void_p, _u64p])
 _render_multi = _sig("tmpt_render_multi", ctypes.c_int,
@@ -137,7 +144,8 @@ _unit_sincos = _sig("tmpt_unit_sincos", ctypes.c_int, [ctypes.c_int32, ctypes.c_
 
 #: every symbol include/tmpt.h declares (checked by tests/test_abi.py)
 EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_scene",
-           "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_destroy", "tmpt_scene_hit",
+           "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_create_ex", "tmpt_scene_set_option",
+           "tmpt_scene_get_option", "tmpt_scene_destroy", "tmpt_scene_hit", "tmpt_scene_hit_ranged",
            "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
            "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos")
 
@@ -283,8 +291,10 @@ def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
 
 def _current_stream(device: int):
     """hipStream_t of torch's current stream on `device` (0 = its null stream),
-    or None without torch / a visible GPU."""
-    if torch is None or not torch.cuda.is_available():
+    or None when torch has not initialised its GPU context (a caller whose
+    device buffer does not come from torch has no torch work to wait for, and
+    asking would initialise torch's context)."""
+    if torch is None or not torch.cuda.is_initialized():
         return None
     return int(torch.cuda.current_stream(device).cuda_stream)
 
@@ -299,16 +309,38 @@ def tile_row_to_y(width, height, band_rows, shard, num_shards) -> np.ndarray:
     return np.array([_tile_row_to_y(ctypes.byref(d), r) for r in range(n)], np.int64)
 
 
-class Scene:
-    """Scene (scene.h:17-43): triangles copied to the GPU, LBVH built there
-    (replaces Scene::BuildOctree, scene.cpp:118-126)."""
+def _options_text(options) -> Optional[bytes]:
+    if options is None:
+        return None
+    if isinstance(options, str):
+        return options.encode()
+    return ",".join(f"{k}={v}" for k, v in dict(options).items()).encode()
 
-    def __init__(self, triangles: np.ndarray, device: int = 0):
+
+class Scene:
+    """Scene (scene.h:17-43): triangles copied to the GPU, BVH built there
+    (replaces Scene::BuildOctree, scene.cpp:118-126).
+
+    ``options``: build and render options (include/tmpt.h "Scene options"),
+    a dict or "key=value,..." string, e.g. ``{"builder": "lbvh", "leaf_max": 4}``;
+    render options can also be changed later with :meth:`set_option`."""
+
+    def __init__(self, triangles: np.ndarray, device: int = 0, options=None):
         tris = np.ascontiguousarray(np.asarray(triangles, np.float32).reshape(-1, 9))
         self._h = ctypes.c_void_p()
         self.n = tris.shape[0]
         self.device = device
-        _check(_scene_create(_fp(tris), self.n, device, ctypes.byref(self._h)), "Scene")
+        _check(_scene_create_ex(_fp(tris), self.n, device, _options_text(options), ctypes.byref(self._h)),
+               "Scene")
+
+    def set_option(self, key: str, value: float) -> None:
+        """A render option (include/tmpt.h); applies to the renders after it."""
+        _check(_set_option(self._h, key.encode(), float(value)), f"set_option({key!r})")
+
+    def get_option(self, key: str) -> float:
+        v = ctypes.c_double()
+        _check(_get_option(self._h, key.encode(), ctypes.byref(v)), f"get_option({key!r})")
+        return v.value
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -328,15 +360,24 @@ class Scene:
         self.close()
 
     # -- Scene::HitScene (scene.cpp:129-140)
-    def hit_scene_batch(self, rays: np.ndarray, t_min: float, t_max: float,
+    def hit_scene_batch(self, rays: np.ndarray, t_min: Optional[float] = None, t_max: Optional[float] = None,
                         any_hit: bool = False) -> Tuple[np.ndarray, np.ndarray]:
-        """rays [n,6] (orig, dir) -> (ids[n] triangle index or -1, hits[n,7] pos/normal/t)."""
-        rays = np.ascontiguousarray(np.asarray(rays, np.float32).reshape(-1, 6))
+        """rays [n,6] (orig, dir) with one [t_min, t_max] for all, or rays [n,8]
+        (orig, dir, tmin, tmax: the range per ray, as HitScene takes it,
+        scene.h:36-37) with t_min = t_max = None
+        -> (ids[n] triangle index or -1, hits[n,7] pos/normal/t)."""
+        rays = np.asarray(rays, np.float32)
+        ranged = t_min is None and t_max is None
+        rays = np.ascontiguousarray(rays.reshape(-1, 8 if ranged else 6))
         n = rays.shape[0]
         hits = np.zeros((n, 7), np.float32)
         ids = np.full(n, -1, np.int32)
-        _check(_scene_hit(self._h, _fp(rays), n, t_min, t_max, int(any_hit), _fp(hits),
-                          ids.ctypes.data_as(_i32p)), "hit_scene")
+        if ranged:
+            _check(_scene_hit_ranged(self._h, _fp(rays), n, int(any_hit), _fp(hits), ids.ctypes.data_as(_i32p)),
+                   "hit_scene")
+        else:
+            _check(_scene_hit(self._h, _fp(rays), n, t_min, t_max, int(any_hit), _fp(hits),
+                              ids.ctypes.data_as(_i32p)), "hit_scene")
         return ids, hits
 
     def hit_scene(self, orig, direction, t_min: float, t_max: float) -> Tuple[int, Optional[Hit]]:
@@ -358,9 +399,10 @@ class Scene:
         Row 0 is the lowest rendered row (main.cpp:229; flipped on PNG write).
         ``out`` may be a device pointer (int) with tile_rows*width*4 bytes; the
         render then starts after the work already enqueued on ``wait_stream``
-        ("current": torch's current stream on the scene's device, so a fill of
-        ``out`` or a collective still reading it is ordered before the render;
-        an int: a raw hipStream_t; None: no ordering).  The call returns once
+        ("current": torch's current stream on the scene's device when torch's
+        GPU context is up, so a fill of ``out`` or a collective still reading
+        it is ordered before the render; an int: a raw hipStream_t; None: no
+        ordering).  The call returns once
         the frame is complete on the device.
         ``spp_begin``/``spp_count``: one progressive pass (persistent engine,
         pixel seeding) -- see :meth:`trace_progressive`."""
@@ -409,15 +451,19 @@ class Scene:
 
 
 def render_multi(tris: np.ndarray, camera: "Camera", width: int, height: int, spp: int, devices,
-                 seed_mode: int = SEED_PIXEL, engine: int = ENGINE_PERSISTENT) -> Tuple[np.ndarray, int, float]:
-    """One frame over several devices in this process (tmpt_render_multi):
-    returns (rgba[height, width, 4], rays, render seconds).  A device may repeat."""
+                 seed_mode: int = SEED_PIXEL, engine: int = ENGINE_PERSISTENT,
+                 require_rccl: bool = False) -> Tuple[np.ndarray, int, float]:
+    """One frame over several devices in this process (tmpt_render_multi: the
+    tiles gathered to devices[0] by one RCCL gather): returns (rgba[height,
+    width, 4], rays, seconds from the renders' start to the assembled frame).
+    A device may repeat (then the gather is device-to-device copies; with
+    require_rccl that is an error instead)."""
     t = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     devs = (ctypes.c_int32 * len(devices))(*devices)
     img = np.zeros((height, width, 4), np.uint8)
     rays = ctypes.c_uint64()
     secs = ctypes.c_double()
-    d = _desc(width, height, spp, seed_mode, 0, 0, 1, engine)
+    d = _desc(width, height, spp, seed_mode, 0, 0, 1, engine, FLAG_REQUIRE_RCCL if require_rccl else 0)
     cam = camera._to_c()
     _check(_render_multi(t.ctypes.data_as(_f32p), t.shape[0], ctypes.byref(cam), ctypes.byref(d), devs,
                          len(devices), img.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays),

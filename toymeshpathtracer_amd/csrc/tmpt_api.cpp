@@ -1,6 +1,8 @@
 // tmpt_api.cpp -- the C ABI of include/tmpt.h.  Status ints cross the
 // boundary; no exception escapes (every entry point catches).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
@@ -26,7 +28,7 @@ void camera_for_scene(tmpt_camera* cam, f3 sceneMin, f3 sceneMax, int w, int h, 
 int write_png(const char* path, const uint8_t* rgba, int w, int h);
 int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t* d_out,
            uint64_t* ray_count);
-int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
+int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any, bool ranged,
                     float* d_hits, int32_t* d_ids);
 
 // RandomUnitVector's (cos a, sin a) over a key range, as the renderers compute it
@@ -37,6 +39,179 @@ __global__ void k_unit_sincos(uint32_t key0, uint32_t n, float2* out)
     float c, s;
     glibc_sincosf_unit(unit_angle((key0 + i) & 0xFFFFFFu), c, s);
     out[i] = make_float2(c, s);
+}
+
+// ---------------------------------------------------------------- multi-device gather
+// Frame assembly on the root device: the gathered tiles are [rank][max_rows][W]
+// (equal-size padded blocks, as ncclGather delivers them); frame row y belongs
+// to rank y % nd as its tile row y / nd (1-row bands dealt round-robin).
+__global__ void k_assemble_rows(const uint32_t* __restrict__ gathered, int32_t nd, int32_t max_rows, int32_t W,
+                                int32_t H, uint32_t* __restrict__ frame)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)W * H) return;
+    const int32_t y = (int32_t)(i / W), x = (int32_t)(i - (int64_t)y * W);
+    frame[i] = gathered[((int64_t)(y % nd) * max_rows + y / nd) * W + x];
+}
+
+// RCCL, resolved at run time (dlopen of librccl.so.1: in a process where torch
+// already loaded its RCCL the same library is reused, so there is one RCCL and
+// one HIP runtime; the library itself loads without RCCL).
+struct Rccl {
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                           hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    bool ok = false;
+};
+
+const Rccl& rccl()
+{
+    static Rccl r = []() {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.comm_init_all = (decltype(x.comm_init_all))dlsym(h, "ncclCommInitAll");
+        x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+        x.gather = (decltype(x.gather))dlsym(h, "ncclGather");
+        x.reduce = (decltype(x.reduce))dlsym(h, "ncclReduce");
+        x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+        x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+        x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+        x.ok = x.comm_init_all && x.comm_destroy && x.gather && x.reduce && x.group_start && x.group_end &&
+               x.error_string;
+        return x;
+    }();
+    return r;
+}
+
+// ---------------------------------------------------------------- options
+// The keys of include/tmpt.h "Scene options", in one table: name, build-time
+// or not, range, and the member they set.
+namespace {
+struct OptionDef {
+    const char* name;
+    bool build;
+    double lo, hi;
+    int Options::*i;
+    float Options::*f;
+    double Options::*d;
+};
+const OptionDef kOptions[] = {
+    {"builder", true, 0, 1, &Options::builder, nullptr, nullptr},
+    {"leaf_max", true, 1, kLeafMaxTris, &Options::leaf_max, nullptr, nullptr},
+    {"collapse", true, 0, 1, &Options::collapse, nullptr, nullptr},
+    {"ploc_radius", true, 1, 256, &Options::ploc_radius, nullptr, nullptr},
+    {"sah_c_leaf", true, 0, 1e6, nullptr, &Options::sah_c_leaf, nullptr},
+    {"sah_c_tri", true, 0, 1e6, nullptr, &Options::sah_c_tri, nullptr},
+    {"sample_block", false, 0, 1024, &Options::sample_block, nullptr, nullptr},
+    {"sbuf_max", false, 0, 1e18, nullptr, nullptr, &Options::sbuf_max},
+    {"pilot", false, -1, 512, &Options::pilot, nullptr, nullptr},
+    {"help", false, -1, 1, &Options::help, nullptr, nullptr},
+    {"pair", false, -1, 63, &Options::pair, nullptr, nullptr},
+    {"balance", false, 0, 1, &Options::balance, nullptr, nullptr},
+    {"dprio", false, 0, 1, &Options::dprio, nullptr, nullptr},
+    {"wave_cap", false, 0, 64, &Options::wave_cap, nullptr, nullptr},
+    {"rowspec", false, 0, 1, &Options::rowspec, nullptr, nullptr},
+    {"rowspec_wmax", false, 0, 16384, &Options::rowspec_wmax, nullptr, nullptr},
+    {"rowspec_windows", false, 0, 32, &Options::rowspec_windows, nullptr, nullptr},
+    {"rowspec_spread", false, -1, 100, nullptr, &Options::rowspec_spread, nullptr},
+    {"rowspec_groups", false, 1, kRowSpecMaxGroups, &Options::rowspec_groups, nullptr, nullptr},
+    {"rowspec_noshadow", false, 0, 1, &Options::rowspec_noshadow, nullptr, nullptr},
+};
+
+const OptionDef* find_option(const char* key)
+{
+    for (const OptionDef& d : kOptions)
+        if (strcmp(d.name, key) == 0) return &d;
+    return nullptr;
+}
+}  // namespace
+
+int options_set(Options& o, const char* key, double v, bool allow_build)
+{
+    const OptionDef* d = key ? find_option(key) : nullptr;
+    if (!d) {
+        set_error(std::string("unknown option '") + (key ? key : "(null)") + "'");
+        return -22;
+    }
+    if (d->build && !allow_build) {
+        set_error(std::string("option '") + key + "' is a build option: give it to tmpt_scene_create_ex");
+        return -22;
+    }
+    if (!(v >= d->lo && v <= d->hi)) {
+        set_error(std::string("option '") + key + "' out of range [" + std::to_string(d->lo) + ", " +
+                  std::to_string(d->hi) + "]");
+        return -22;
+    }
+    if (d->i) {
+        if (v != (double)(long long)v) {
+            set_error(std::string("option '") + key + "' takes an integer");
+            return -22;
+        }
+        if (strcmp(key, "sample_block") == 0 && v > 0 && ((long long)v & ((long long)v - 1)) != 0) {
+            set_error("option 'sample_block' must be a power of two (or 0 = auto)");
+            return -22;
+        }
+        o.*(d->i) = (int)v;
+    } else if (d->f) {
+        o.*(d->f) = (float)v;
+    } else {
+        o.*(d->d) = v;
+    }
+    return 0;
+}
+
+int options_get(const Options& o, const char* key, double* v)
+{
+    const OptionDef* d = key ? find_option(key) : nullptr;
+    if (!d) {
+        set_error(std::string("unknown option '") + (key ? key : "(null)") + "'");
+        return -22;
+    }
+    *v = d->i ? (double)(o.*(d->i)) : d->f ? (double)(o.*(d->f)) : o.*(d->d);
+    return 0;
+}
+
+// "key=value,key=value" (spaces allowed); builder=ploc|lbvh and
+// collapse=greedy|sah also take their names
+int options_parse(Options& o, const char* text, bool allow_build)
+{
+    if (!text) return 0;
+    std::string t(text);
+    size_t pos = 0;
+    while (pos <= t.size()) {
+        size_t end = t.find(',', pos);
+        if (end == std::string::npos) end = t.size();
+        std::string item = t.substr(pos, end - pos);
+        pos = end + 1;
+        item.erase(0, item.find_first_not_of(" \t"));
+        item.erase(item.find_last_not_of(" \t") + 1);
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) {
+            set_error("option '" + item + "' has no value (key=value)");
+            return -22;
+        }
+        std::string key = item.substr(0, eq), val = item.substr(eq + 1);
+        key.erase(key.find_last_not_of(" \t") + 1);
+        val.erase(0, val.find_first_not_of(" \t"));
+        if (key == "builder" && (val == "ploc" || val == "lbvh")) val = val == "lbvh" ? "1" : "0";
+        if (key == "collapse" && (val == "greedy" || val == "sah")) val = val == "sah" ? "1" : "0";
+        char* endp = nullptr;
+        const double v = strtod(val.c_str(), &endp);
+        if (val.empty() || !endp || *endp != '\0') {
+            set_error("option '" + key + "': bad value '" + val + "'");
+            return -22;
+        }
+        if (int rc = options_set(o, key.c_str(), v, allow_build)) return rc;
+    }
+    return 0;
 }
 
 }  // namespace tmpt
@@ -149,15 +324,26 @@ int tmpt_device_count(void)
 
 int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene** out)
 {
+    return tmpt_scene_create_ex(tris, n, device, nullptr, out);
+}
+
+int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out)
+{
     TMPT_GUARD_BEGIN
     if (!out || n < 0 || (n > 0 && !tris)) return bad("tmpt_scene_create: bad arguments");
     *out = nullptr;
+    Options opt;
+    if (int rc = options_parse(opt, options, true)) {
+        set_error(std::string("tmpt_scene_create: ") + last_error());
+        return rc;
+    }
     int ndev = 0;
     TMPT_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return bad("tmpt_scene_create: no such device");
     TMPT_HIP(hipSetDevice(device));
     tmpt_scene* h = new tmpt_scene();
     Scene& s = h->s;
+    s.opt = opt;
     s.device = device;
     s.n = n;
     auto fail = [&](int rc) {
@@ -178,12 +364,6 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
     int rc = build_lbvh(s, d_tris);
     if (d_tris) (void)hipFree(d_tris);
     if (rc) return fail(rc);
-    {
-        auto t0 = std::chrono::steady_clock::now();
-        rc = build_shadow_grid(s, tris);
-        if (rc) return fail(rc);
-        s.build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
     *out = h;
     return 0;
     TMPT_GUARD_END
@@ -197,9 +377,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     for (auto& st : s.rs_stream)  // the speculative row engine's group streams
         if (st) (void)hipStreamSynchronize(st);
-    if (s.nodes) (void)hipFree(s.nodes);
     if (s.nodes4) (void)hipFree(s.nodes4);
-    if (s.nodes4f) (void)hipFree(s.nodes4f);
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);
@@ -211,7 +389,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
         if (ev) (void)hipEventDestroy(ev);
     if (s.rs_host) (void)hipHostFree(s.rs_host);
     if (s.rs_list) (void)hipFree(s.rs_list);
-    free_shadow_grid(s);
+    if (s.wait_ev) (void)hipEventDestroy(s.wait_ev);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);
@@ -222,12 +400,30 @@ int tmpt_scene_destroy(tmpt_scene* h)
     return 0;
 }
 
-int tmpt_scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, float tmax,
-                   int32_t any_hit, float* hits, int32_t* ids)
+int tmpt_scene_set_option(tmpt_scene* h, const char* key, double value)
 {
     TMPT_GUARD_BEGIN
+    if (!h) return bad("tmpt_scene_set_option: null scene");
+    return options_set(h->s.opt, key, value, false);
+    TMPT_GUARD_END
+}
+
+int tmpt_scene_get_option(const tmpt_scene* h, const char* key, double* value)
+{
+    TMPT_GUARD_BEGIN
+    if (!h || !value) return bad("tmpt_scene_get_option: null argument");
+    return options_get(h->s.opt, key, value);
+    TMPT_GUARD_END
+}
+
+namespace {
+// the batched HitScene: stride 6 (one range) or 8 (per-ray tmin, tmax)
+int scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, float tmax, bool ranged,
+              int32_t any_hit, float* hits, int32_t* ids)
+{
     if (!hc || n < 0 || (n > 0 && (!rays || !hits || !ids))) return bad("tmpt_scene_hit: bad arguments");
     if (n == 0) return 0;
+    const size_t rs = ranged ? 32 : 24;
     Scene& s = const_cast<tmpt_scene*>(hc)->s;
     TMPT_HIP(hipSetDevice(s.device));
     float *d_rays = nullptr, *d_hits = nullptr;
@@ -237,22 +433,38 @@ int tmpt_scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmi
         if (d_hits) (void)hipFree(d_hits);
         if (d_ids) (void)hipFree(d_ids);
     };
-    if (hipMalloc(&d_rays, 24 * (size_t)n) != hipSuccess || hipMalloc(&d_hits, 28 * (size_t)n) != hipSuccess ||
+    if (hipMalloc(&d_rays, rs * (size_t)n) != hipSuccess || hipMalloc(&d_hits, 28 * (size_t)n) != hipSuccess ||
         hipMalloc(&d_ids, 4 * (size_t)n) != hipSuccess) {
         cleanup();
         return bad("tmpt_scene_hit: out of device memory");
     }
     int rc = 0;
-    if (hipMemcpy(d_rays, rays, 24 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(d_rays, rays, rs * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_hits, hits, 28 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
         rc = (set_error("tmpt_scene_hit: upload failed"), -1);
-    if (!rc) rc = intersect_batch(s, d_rays, n, tmin, tmax, any_hit != 0, d_hits, d_ids);
+    if (!rc) rc = intersect_batch(s, d_rays, n, tmin, tmax, any_hit != 0, ranged, d_hits, d_ids);
     if (!rc && (hipStreamSynchronize(s.stream) != hipSuccess ||
                 hipMemcpy(hits, d_hits, 28 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(ids, d_ids, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
         rc = (set_error("tmpt_scene_hit: kernel or readback failed"), -1);
     cleanup();
     return rc;
+}
+}  // namespace
+
+int tmpt_scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, float tmax,
+                   int32_t any_hit, float* hits, int32_t* ids)
+{
+    TMPT_GUARD_BEGIN
+    return scene_hit(hc, rays, n, tmin, tmax, false, any_hit, hits, ids);
+    TMPT_GUARD_END
+}
+
+int tmpt_scene_hit_ranged(const tmpt_scene* hc, const float* rays8, int64_t n, int32_t any_hit, float* hits,
+                          int32_t* ids)
+{
+    TMPT_GUARD_BEGIN
+    return scene_hit(hc, rays8, n, 0.0f, 0.0f, true, any_hit, hits, ids);
     TMPT_GUARD_END
 }
 
@@ -324,12 +536,54 @@ int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, cons
     TMPT_GUARD_BEGIN
     if (!cam || !desc || !devices || ndevices < 1 || !rgba_full || (n > 0 && !tris))
         return bad("tmpt_render_multi: bad arguments");
+    if (desc->width < 1 || desc->width > 10000 || desc->height < 1 || desc->height > 10000)
+        return bad("tmpt_render_multi: invalid width / height");
     const int nd = ndevices;
+    const int W = desc->width, H = desc->height;
+    bool unique = true;
+    for (int g = 0; g < nd; ++g)
+        for (int k = 0; k < g; ++k) unique = unique && devices[g] != devices[k];
+    const bool use_rccl = unique && rccl().ok;
+    if ((desc->flags & TMPT_FLAG_REQUIRE_RCCL) && !use_rccl)
+        return bad(unique ? "tmpt_render_multi: RCCL (librccl.so.1) not available"
+                          : "tmpt_render_multi: RCCL needs distinct devices (a device is listed twice)");
     std::vector<tmpt_scene*> scenes((size_t)nd, nullptr);
     std::vector<int> rcs((size_t)nd, 0);
     std::vector<std::string> errs((size_t)nd);
-    auto destroy_all = [&]() {
+    // per rank: its padded tile and ray count on its device; on rank 0 also the
+    // gathered tiles, the frame and the summed count
+    const int max_rows = (H + nd - 1) / nd;
+    const size_t tile_bytes = (size_t)max_rows * (size_t)W * 4;
+    std::vector<uint8_t*> d_tile((size_t)nd, nullptr);
+    std::vector<uint64_t*> d_rays((size_t)nd, nullptr);
+    std::vector<hipStream_t> streams((size_t)nd, nullptr);
+    uint8_t* d_gather = nullptr;
+    uint32_t* d_frame = nullptr;
+    uint64_t* d_total = nullptr;
+    std::vector<ncclComm_t> comms;
+    auto cleanup = [&]() {
+        for (int g = 0; g < nd; ++g) {
+            (void)hipSetDevice(devices[g]);
+            if (streams[(size_t)g]) (void)hipStreamSynchronize(streams[(size_t)g]);
+        }
+        for (ncclComm_t c : comms)
+            if (c) (void)rccl().comm_destroy(c);
+        for (int g = 0; g < nd; ++g) {
+            (void)hipSetDevice(devices[g]);
+            if (d_tile[(size_t)g]) (void)hipFree(d_tile[(size_t)g]);
+            if (d_rays[(size_t)g]) (void)hipFree(d_rays[(size_t)g]);
+            if (streams[(size_t)g]) (void)hipStreamDestroy(streams[(size_t)g]);
+        }
+        (void)hipSetDevice(devices[0]);
+        if (d_gather) (void)hipFree(d_gather);
+        if (d_frame) (void)hipFree(d_frame);
+        if (d_total) (void)hipFree(d_total);
         for (auto* sc : scenes) tmpt_scene_destroy(sc);
+    };
+    auto fail = [&](const std::string& msg, int rc) {
+        cleanup();
+        set_error("tmpt_render_multi: " + msg);
+        return rc;
     };
     {  // scene per device, concurrently (error text is thread-local: keep each thread's)
         std::vector<std::thread> th;
@@ -341,49 +595,91 @@ int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, cons
         for (auto& t : th) t.join();
     }
     for (int g = 0; g < nd; ++g)
-        if (rcs[(size_t)g]) {
-            destroy_all();
-            return (set_error("tmpt_render_multi: " + errs[(size_t)g]), rcs[(size_t)g]);
-        }
-    std::vector<tmpt_render_desc> ds((size_t)nd, *desc);
-    std::vector<std::vector<uint8_t>> tiles((size_t)nd);
-    std::vector<uint64_t> rays((size_t)nd, 0);
+        if (rcs[(size_t)g]) return fail(errs[(size_t)g], rcs[(size_t)g]);
     for (int g = 0; g < nd; ++g) {
-        tmpt_render_desc& d = ds[(size_t)g];
-        d.band_rows = nd > 1 ? 1 : desc->band_rows;  // rows dealt round-robin: balanced shards
-        d.shard = g;
-        d.num_shards = nd;
-        d.flags = 0;
-        tiles[(size_t)g].resize((size_t)std::max(0, tmpt_tile_rows(&d)) * (size_t)std::max(0, d.width) * 4);
+        if (hipSetDevice(devices[g]) != hipSuccess || hipStreamCreateWithFlags(&streams[(size_t)g], hipStreamNonBlocking) ||
+            hipMalloc(&d_tile[(size_t)g], tile_bytes) != hipSuccess ||
+            hipMalloc(&d_rays[(size_t)g], sizeof(uint64_t)) != hipSuccess ||
+            hipMemsetAsync(d_tile[(size_t)g], 0, tile_bytes, streams[(size_t)g]) != hipSuccess)
+            return fail("out of device memory", -1);
     }
+    if (hipSetDevice(devices[0]) != hipSuccess || hipMalloc(&d_gather, tile_bytes * (size_t)nd) != hipSuccess ||
+        hipMalloc(&d_frame, (size_t)W * H * 4) != hipSuccess || hipMalloc(&d_total, sizeof(uint64_t)) != hipSuccess)
+        return fail("out of device memory (root)", -1);
+    if (use_rccl) {  // single-process form of SURVEY.md §8e: one communicator per device
+        comms.assign((size_t)nd, nullptr);
+        const ncclResult_t r = rccl().comm_init_all(comms.data(), nd, devices);
+        if (r != ncclSuccess) {
+            comms.clear();
+            return fail(std::string("ncclCommInitAll: ") + rccl().error_string(r), -1);
+        }
+    }
+    for (int g = 0; g < nd; ++g) (void)hipStreamSynchronize(streams[(size_t)g]);
+    std::vector<tmpt_render_desc> ds((size_t)nd, *desc);
+    std::vector<uint64_t> rays((size_t)nd, 0);
     const auto t0 = std::chrono::steady_clock::now();
-    {
+    {  // every device renders its rows into its device tile, one host thread each
         std::vector<std::thread> th;
         for (int g = 0; g < nd; ++g)
             th.emplace_back([&, g]() {
-                rcs[(size_t)g] = tmpt_render(scenes[(size_t)g], cam, &ds[(size_t)g], tiles[(size_t)g].data(),
-                                             &rays[(size_t)g]);
+                tmpt_render_desc& d = ds[(size_t)g];
+                d.band_rows = 1;  // rows dealt round-robin: statistically equal shards
+                d.shard = g;
+                d.num_shards = nd;
+                d.flags = TMPT_FLAG_OUT_DEVICE;
+                rcs[(size_t)g] = tmpt_render(scenes[(size_t)g], cam, &d, d_tile[(size_t)g], &rays[(size_t)g]);
                 if (rcs[(size_t)g]) errs[(size_t)g] = tmpt_last_error();
+                else if (hipSetDevice(devices[g]) != hipSuccess ||
+                         hipMemcpyAsync(d_rays[(size_t)g], &rays[(size_t)g], sizeof(uint64_t), hipMemcpyHostToDevice,
+                                        streams[(size_t)g]) != hipSuccess ||
+                         hipStreamSynchronize(streams[(size_t)g]) != hipSuccess)
+                    rcs[(size_t)g] = -1, errs[(size_t)g] = "ray count upload failed";
             });
         for (auto& t : th) t.join();
     }
-    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int g = 0; g < nd; ++g)
+        if (rcs[(size_t)g]) return fail(errs[(size_t)g], rcs[(size_t)g]);
     uint64_t total = 0;
-    for (int g = 0; g < nd; ++g) {
-        if (rcs[(size_t)g]) {
-            destroy_all();
-            return (set_error("tmpt_render_multi: " + errs[(size_t)g]), rcs[(size_t)g]);
+    if (use_rccl) {
+        // ONE gather of the equal-size padded tiles to device 0 over xGMI and a
+        // uint64 sum of the ray counts, grouped (one thread drives every device)
+        ncclResult_t r = rccl().group_start();
+        for (int g = 0; g < nd && r == ncclSuccess; ++g) {
+            r = rccl().gather(d_tile[(size_t)g], g == 0 ? d_gather : nullptr, tile_bytes, ncclUint8, 0,
+                              comms[(size_t)g], streams[(size_t)g]);
+            if (r == ncclSuccess)
+                r = rccl().reduce(d_rays[(size_t)g], g == 0 ? d_total : nullptr, 1, ncclUint64, ncclSum, 0,
+                                  comms[(size_t)g], streams[(size_t)g]);
         }
-        total += rays[(size_t)g];
-        const tmpt_render_desc& d = ds[(size_t)g];
-        const int rows = tmpt_tile_rows(&d);
-        for (int r = 0; r < rows; ++r) {
-            const int y = tmpt_tile_row_to_y(&d, r);
-            memcpy(rgba_full + (size_t)y * d.width * 4, tiles[(size_t)g].data() + (size_t)r * d.width * 4,
-                   (size_t)d.width * 4);
+        const ncclResult_t re = rccl().group_end();
+        if (r == ncclSuccess) r = re;
+        if (r != ncclSuccess) return fail(std::string("RCCL gather: ") + rccl().error_string(r), -1);
+        for (int g = 0; g < nd; ++g)
+            if (hipSetDevice(devices[g]) != hipSuccess || hipStreamSynchronize(streams[(size_t)g]) != hipSuccess)
+                return fail("gather failed", -1);
+        (void)hipSetDevice(devices[0]);
+        if (hipMemcpy(&total, d_total, sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail("ray count readback failed", -1);
+    } else {
+        // a device listed more than once (RCCL ranks need distinct devices):
+        // the same gather as device-to-device copies into the root's buffer
+        (void)hipSetDevice(devices[0]);
+        for (int g = 0; g < nd; ++g) {
+            if (hipMemcpyPeerAsync(d_gather + (size_t)g * tile_bytes, devices[0], d_tile[(size_t)g], devices[g],
+                                   tile_bytes, streams[0]) != hipSuccess)
+                return fail("device-to-device gather failed", -1);
+            total += rays[(size_t)g];
         }
     }
-    destroy_all();
+    (void)hipSetDevice(devices[0]);
+    k_assemble_rows<<<(unsigned)(((int64_t)W * H + 255) / 256), 256, 0, streams[0]>>>(
+        reinterpret_cast<const uint32_t*>(d_gather), nd, max_rows, W, H, d_frame);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(streams[0]) != hipSuccess)
+        return fail("frame assembly failed", -1);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (hipMemcpy(rgba_full, d_frame, (size_t)W * H * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("frame readback failed", -1);
+    cleanup();
     if (ray_count) *ray_count = total;
     if (seconds) *seconds = dt;
     return 0;

@@ -13,8 +13,13 @@
 //   6. k_refit_level  boxes bottom-up, one launch per level: the kernel boundary
 //                     is the only inter-workgroup synchronisation, so no
 //                     cross-XCD release/acquire is needed
-//   7. k_assemble     64-B nodes (both child boxes + child links) and the
-//                     leaf-ordered TriPre records
+//   or, the default, PLOC (Meister & Bittner 2018) over the same sorted keys:
+//      k_ploc_nn / k_ploc_merge / k_ploc_compact per iteration, then
+//      top-down leaf numbering (k_ploc_offsets / relabel / vals)
+//   7. k_tri_pre      leaf-ordered TriPre records
+//   8. k_bvh4_level   top-down collapse to the 4-wide quantised BVH, one launch
+//                     per level (greedy largest-area opening, or the SAH-optimal
+//                     forests of k_sah_level)
 // The build is outside the timed region of the reference (main.cpp:312 vs
 // :319) and of bench.py; it is timed separately (Scene::build_ms).
 #include <hip/hip_runtime.h>
@@ -297,23 +302,6 @@ __global__ void __launch_bounds__(kBlock) k_refit_level(const int2* __restrict__
     ib.hx[i] = fmaxf(a[3], b[3]); ib.hy[i] = fmaxf(a[4], b[4]); ib.hz[i] = fmaxf(a[5], b[5]);
 }
 
-__global__ void __launch_bounds__(kBlock) k_assemble(const int2* __restrict__ child,
-                                                     const int32_t* __restrict__ depth, int32_t m,
-                                                     Soa6 leaf, const uint32_t* __restrict__ vals,
-                                                     Soa6 ib, BvhNode* __restrict__ nodes)
-{
-    int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= m) return;
-    int2 c = child[i];
-    float a[6], b[6];
-    child_box(c.x, leaf, vals, ib, a);
-    child_box(c.y, leaf, vals, ib, b);
-    nodes[i].a = f4(a[0], a[1], a[2], a[3]);
-    nodes[i].b = f4(a[4], a[5], b[0], b[1]);
-    nodes[i].c = f4(b[2], b[3], b[4], b[5]);
-    nodes[i].d = make_int4(c.x, c.y, depth[i], 0);
-}
-
 // ---------------------------------------------------------------- PLOC
 // Parallel Locally-Ordered Clustering (Meister & Bittner, TVCG 2018) over the
 // Morton order: every cluster finds its nearest neighbour (smallest union
@@ -447,152 +435,6 @@ __device__ __forceinline__ float box_area(const float b[6])
     return dx * dy + dy * dz + dz * dx;
 }
 
-__device__ __forceinline__ float box_area6(const Soa6& ib, int k)
-{
-    float dx = ib.hx[k] - ib.lx[k], dy = ib.hy[k] - ib.ly[k], dz = ib.hz[k] - ib.lz[k];
-    return dx * dy + dy * dz + dz * dx;
-}
-
-// ---------------------------------------------------------------- treelet restructuring
-// Karras & Aila, "Fast Parallel Construction of High-Quality Bounding Volume
-// Hierarchies" (HPG 2013): a treelet = a node R and the internal nodes below
-// it opened largest-area first until it has kTreeletLeaves leaves (subtrees).
-// A dynamic programme over the 2^n leaf subsets finds the binary topology of
-// least summed internal-node area (the SAH with the leaves' subtrees fixed);
-// the treelet's internal nodes are rewired to it (R keeps its index, so the
-// tree above is untouched).  One thread per treelet; the treelets of one BFS
-// level are disjoint subtrees, levels go deepest first, one launch each.
-constexpr int kTreeletLeaves = 7;
-
-__global__ void __launch_bounds__(64) k_treelet(const int32_t* __restrict__ list, int nl, int2* __restrict__ child,
-                                                Soa6 leaf, const uint32_t* __restrict__ vals, Soa6 ib,
-                                                int32_t* __restrict__ size, int min_size,
-                                                unsigned long long* __restrict__ stats)
-{
-    const int i = (int)(blockIdx.x * 64 + threadIdx.x);
-    if (i >= nl) return;
-    const int R = list[i];
-    if (size[R] < min_size) return;
-    int T[kTreeletLeaves], I[kTreeletLeaves - 1], ts[kTreeletLeaves];
-    float tb[kTreeletLeaves][6];
-    const int2 c0 = child[R];
-    T[0] = c0.x;
-    T[1] = c0.y;
-    I[0] = R;
-    int nt = 2, ni = 1;
-    child_box(T[0], leaf, vals, ib, tb[0]);
-    child_box(T[1], leaf, vals, ib, tb[1]);
-    float orig = box_area6(ib, R);
-    while (nt < kTreeletLeaves) {
-        int best = -1;
-        float ba = -1.0f;
-        for (int k = 0; k < nt; ++k)
-            if (T[k] >= 0) {
-                const float a = box_area(tb[k]);
-                if (a > ba) { ba = a; best = k; }
-            }
-        if (best < 0) break;
-        const int x = T[best];
-        orig += ba;
-        I[ni++] = x;
-        const int2 cc = child[x];
-        T[best] = cc.x;
-        child_box(cc.x, leaf, vals, ib, tb[best]);
-        T[nt] = cc.y;
-        child_box(cc.y, leaf, vals, ib, tb[nt]);
-        ++nt;
-    }
-    if (nt < 3) return;  // a single internal node: nothing to choose
-    for (int k = 0; k < nt; ++k) ts[k] = T[k] < 0 ? 1 : size[T[k]];
-    const int full = (1 << nt) - 1;
-    float C[1 << kTreeletLeaves];
-    uint8_t PB[1 << kTreeletLeaves];
-    for (int S = 1; S <= full; ++S) {
-        if ((S & (S - 1)) == 0) {
-            C[S] = 0.0f;
-            PB[S] = 0;
-            continue;
-        }
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (int k = 0; k < nt; ++k)
-            if (S >> k & 1)
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = fminf(lo[a], tb[k][a]);
-                    hi[a] = fmaxf(hi[a], tb[k][3 + a]);
-                }
-        const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-        const float area = dx * dy + dy * dz + dz * dx;
-        // subsets below S are final (increasing S); P holds S's lowest leaf, so
-        // each split is seen once
-        const int low = S & -S;
-        float best = INFINITY;
-        int bp = 0;
-        for (int P = (S - 1) & S; P; P = (P - 1) & S) {
-            if (!(P & low)) continue;
-            const float v = C[P] + C[S ^ P];
-            if (v < best) { best = v; bp = P; }
-        }
-        C[S] = area + best;
-        PB[S] = (uint8_t)bp;
-    }
-    if (!(C[full] < orig * (1.0f - 1e-5f))) return;
-    // rewire: (subset, node) pairs, R first, the other internal nodes reused in order
-    int stS[kTreeletLeaves], stN[kTreeletLeaves], sp = 0, next = 1;
-    stS[sp] = full;
-    stN[sp] = R;
-    ++sp;
-    while (sp > 0) {
-        --sp;
-        const int S = stS[sp], id = stN[sp];
-        const int P = PB[S], Q = S ^ P;
-        int ch[2];
-        const int sub[2] = {P, Q};
-        for (int h = 0; h < 2; ++h) {
-            if ((sub[h] & (sub[h] - 1)) == 0) {
-                ch[h] = T[__builtin_ctz(sub[h])];
-            } else {
-                ch[h] = I[next++];
-                stS[sp] = sub[h];
-                stN[sp] = ch[h];
-                ++sp;
-            }
-        }
-        child[id] = make_int2(ch[0], ch[1]);
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        int cnt = 0;
-        for (int k = 0; k < nt; ++k)
-            if (S >> k & 1) {
-                cnt += ts[k];
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = fminf(lo[a], tb[k][a]);
-                    hi[a] = fmaxf(hi[a], tb[k][3 + a]);
-                }
-            }
-        ib.lx[id] = lo[0]; ib.ly[id] = lo[1]; ib.lz[id] = lo[2];
-        ib.hx[id] = hi[0]; ib.hy[id] = hi[1]; ib.hz[id] = hi[2];
-        size[id] = cnt;
-    }
-    if (stats) atomicAdd(stats, 1ull);
-}
-
-// top-down leaf offsets over one BFS level of an arbitrary binary tree (the
-// restructured one: PLOC's creation iterations no longer order it)
-__global__ void __launch_bounds__(kBlock) k_offsets_list(const int32_t* __restrict__ list, int nl,
-                                                         const int2* __restrict__ child,
-                                                         const int32_t* __restrict__ size,
-                                                         int32_t* __restrict__ off,
-                                                         uint32_t* __restrict__ new_slot)
-{
-    const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (i >= nl) return;
-    const int k = list[i];
-    const int o = off[k];
-    const int2 c = child[k];
-    const int s0 = c.x < 0 ? 1 : size[c.x];
-    if (c.x >= 0) off[c.x] = o; else new_slot[~c.x] = (uint32_t)o;
-    if (c.y >= 0) off[c.y] = o + s0; else new_slot[~c.y] = (uint32_t)(o + s0);
-}
-
 __device__ __forceinline__ void node_or_leaf_box(int c, const Soa6& leaf,
                                                  const uint32_t* __restrict__ vals, const Soa6& ib,
                                                  float b[6])
@@ -717,8 +559,7 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
                                                        const int2* __restrict__ frontier, int nf,
                                                        int2* __restrict__ next,
                                                        uint32_t* __restrict__ counters,
-                                                       Bvh4Node* __restrict__ out,
-                                                       Bvh4FNode* __restrict__ outf, int leaf_max,
+                                                       Bvh4Node* __restrict__ out, int leaf_max,
                                                        int n_tris, const uint32_t* __restrict__ dec)
 {
     int i = blockIdx.x * kBlock + threadIdx.x;
@@ -808,95 +649,10 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
             lk[k] = (int)slot;
         }
     }
-    {
-        float pl[6][4];
-        for (int k = 0; k < 4; ++k)
-            for (int a = 0; a < 3; ++a) {
-                pl[2 * a][k] = k < nc ? bx[k][a] : INFINITY;
-                pl[2 * a + 1][k] = k < nc ? bx[k][3 + a] : -INFINITY;
-            }
-        for (int j = 0; j < 6; ++j) outf[dst].p[j] = f4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
-        outf[dst].links = links;
-        outf[dst].pad = make_int4(0, 0, 0, 0);
-    }
     out[dst].a = f4(lo[0], lo[1], lo[2], __uint_as_float(ebits | (mask << 24)));
     out[dst].b = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
     out[dst].c = make_uint4(qlo[2], qhi[2], 0u, 0u);
     out[dst].d = links;
-}
-
-// Node layout pass (TMPT_LAYOUT=1): the first kTopNodes nodes keep their
-// level-order slots (the path kernel copies them to LDS); below them every
-// node's internal children get consecutive slots (a sibling block: 4 children
-// = 2 lines), and each child's subtree follows its block depth first.
-// desc[n] = internal nodes strictly below n; one launch per level, deepest first.
-__global__ void __launch_bounds__(kBlock) k_desc_level(const Bvh4Node* __restrict__ nodes, int lo, int hi,
-                                                      int32_t* __restrict__ desc)
-{
-    const int n = lo + (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (n >= hi) return;
-    const int4 L = nodes[n].d;
-    const int c[4] = {L.x, L.y, L.z, L.w};
-    int d = 0;
-    for (int k = 0; k < 4; ++k)
-        if (c[k] >= 0) d += 1 + desc[c[k]];
-    desc[n] = d;
-}
-
-// children-block starts of the top nodes: the region past the top is dealt
-// out to them in slot order (one thread: at most kTopNodes nodes)
-__global__ void k_top_blocks(const Bvh4Node* __restrict__ nodes, int ntop, const int32_t* __restrict__ desc,
-                             int32_t* __restrict__ cb, int32_t* __restrict__ newidx)
-{
-    int next = ntop;
-    for (int t = 0; t < ntop; ++t) {
-        newidx[t] = t;
-        cb[t] = next;
-        const int4 L = nodes[t].d;
-        const int c[4] = {L.x, L.y, L.z, L.w};
-        for (int k = 0; k < 4; ++k)
-            if (c[k] >= ntop) next += 1 + desc[c[k]];
-    }
-}
-
-// one level, top down: node n's non-top internal children take slots
-// cb[n], cb[n]+1, ...; child i's own block starts after the sibling block and
-// the subtrees of children 0..i-1
-__global__ void __launch_bounds__(kBlock) k_place_level(const Bvh4Node* __restrict__ nodes, int lo, int hi,
-                                                       int ntop, const int32_t* __restrict__ desc,
-                                                       int32_t* __restrict__ cb, int32_t* __restrict__ newidx)
-{
-    const int n = lo + (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (n >= hi) return;
-    const int4 L = nodes[n].d;
-    const int c[4] = {L.x, L.y, L.z, L.w};
-    const int b = cb[n];
-    int k = 0;
-    for (int j = 0; j < 4; ++j) k += c[j] >= ntop;
-    int slot = b, sub = b + k;
-    for (int j = 0; j < 4; ++j) {
-        if (c[j] < ntop) continue;
-        newidx[c[j]] = slot++;
-        cb[c[j]] = sub;
-        sub += desc[c[j]];
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) k_relayout(const Bvh4Node* __restrict__ in, const Bvh4FNode* __restrict__ inf,
-                                                    int n4, const int32_t* __restrict__ newidx,
-                                                    Bvh4Node* __restrict__ out, Bvh4FNode* __restrict__ outf)
-{
-    const int n = (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (n >= n4) return;
-    const int d = newidx[n];
-    Bvh4Node q = in[n];
-    int* c = &q.d.x;
-    for (int k = 0; k < 4; ++k)
-        if (c[k] >= 0) c[k] = newidx[c[k]];
-    out[d] = q;
-    Bvh4FNode f = inf[n];
-    f.links = q.d;
-    outf[d] = f;
 }
 
 __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tris9, int32_t n,
@@ -912,15 +668,6 @@ __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tr
     pre[k].a = f4(v0.x, v0.y, v0.z, e1.x);
     pre[k].b = f4(e1.y, e1.z, e2.x, e2.y);
     pre[k].c = f4(e2.z, __int_as_float(o), 0.0f, 0.0f);
-}
-
-// single-triangle scene: one node whose two children are the same leaf
-__global__ void k_single(Soa6 leaf, BvhNode* nodes)
-{
-    nodes[0].a = f4(leaf.lx[0], leaf.ly[0], leaf.lz[0], leaf.hx[0]);
-    nodes[0].b = f4(leaf.hy[0], leaf.hz[0], leaf.lx[0], leaf.ly[0]);
-    nodes[0].c = f4(leaf.lz[0], leaf.hx[0], leaf.hy[0], leaf.hz[0]);
-    nodes[0].d = make_int4(~0, ~0, 0, 0);
 }
 
 inline int blocks_for(int64_t n, int b) { return (int)((n + b - 1) / b); }
@@ -956,16 +703,14 @@ int build_lbvh(Scene& s, const float* d_tris9)
     auto t0 = std::chrono::steady_clock::now();
     const int32_t m = n >= 2 ? n - 1 : 1;  // internal nodes
     s.n_nodes = m;
-    TMPT_HIP(hipMalloc(&s.nodes, sizeof(BvhNode) * (size_t)m));
     TMPT_HIP(hipMalloc(&s.nodes4, sizeof(Bvh4Node) * (size_t)m));
-    TMPT_HIP(hipMalloc(&s.nodes4f, sizeof(Bvh4FNode) * (size_t)m));
     // one extra slot: the null triangle (all zero: det = 0, never accepted) that
     // empty BVH4 child slots link to
     TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * ((size_t)n + 1)));
     TMPT_HIP(hipMemsetAsync(s.tri_pre + n, 0, sizeof(TriPre), st));
     TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(n, 1)));
     if (n == 0) {
-        TMPT_HIP(hipMemsetAsync(s.nodes, 0, sizeof(BvhNode), st));
+        TMPT_HIP(hipMemsetAsync(s.nodes4, 0, sizeof(Bvh4Node), st));
         s.max_depth = 0;
         return 0;
     }
@@ -1027,11 +772,8 @@ int build_lbvh(Scene& s, const float* d_tris9)
             std::swap(vi, vo);
         }
         // sorted (ki, vi)
-        const char* bname = getenv("TMPT_BUILDER");
-        const bool ploc = !(bname && std::string(bname) == "lbvh") && n > 1;
-        s.has_bvh2 = !ploc;
+        const bool ploc = s.opt.builder == 0 && n > 1;
         if (n == 1) {
-            k_single<<<1, 1, 0, st>>>(leaf, s.nodes);
             s.max_depth = 0;
         } else {
             k_karras<<<blocks_for(m, kBlock), kBlock, 0, st>>>(ki, n, child, range, pint, pleaf);
@@ -1047,7 +789,6 @@ int build_lbvh(Scene& s, const float* d_tris9)
         }
             for (int L = hmax; L >= 0; --L)
                 k_refit_level<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, L, leaf, vi, ib);
-            k_assemble<<<blocks_for(m, kBlock), kBlock, 0, st>>>(child, depth, m, leaf, vi, ib, s.nodes);
         }
         // binary tree the BVH4Q is collapsed from: the LBVH, or a PLOC tree
         const int2* tchild = child;
@@ -1056,8 +797,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
         const uint32_t* tvals = vi;
         int troot = n == 1 ? ~0 : 0;
         if (ploc) {
-            int r = 32;  // search radius; node visits vs r measured in DESIGN.md
-            if (const char* e = getenv("TMPT_PLOC_R")) r = std::max(1, std::min(256, atoi(e)));
+            const int r = s.opt.ploc_radius;  // search radius; node visits vs r measured in DESIGN.md
             int32_t* cidA = (int32_t*)alloc(nn * 4);
             int32_t* cidB = (int32_t*)alloc(nn * 4);
             float* cbAb = (float*)alloc(6 * nn * 4);
@@ -1107,46 +847,8 @@ int build_lbvh(Scene& s, const float* d_tris9)
                 ++it;
             }
             if (rc) break;
-            int tpass = 0;  // TMPT_TREELET=<passes>: treelet restructuring of the PLOC tree
-            if (const char* e = getenv("TMPT_TREELET")) tpass = std::max(0, std::min(8, atoi(e)));
-            if (tpass > 0 && m >= 2) {
-                int32_t* ord = (int32_t*)alloc(mm * 4);
-                if (!ord) { set_error("build: out of device memory (treelet)"); rc = -1; break; }
-                const int32_t root = m - 1;
-                // BFS levels of the current tree: ord[off[l] .. off[l+1])
-                auto bfs = [&](std::vector<int>& off) -> bool {
-                    off = {0, 1};
-                    uint32_t zero = 0, cnt = 0;
-                    if (hipMemcpyAsync(ord, &root, 4, hipMemcpyHostToDevice, st) != hipSuccess) return false;
-                    while (off.back() > off[off.size() - 2]) {
-                        const int b0 = off[off.size() - 2], b1 = off.back();
-                        if (hipMemcpyAsync(c4, &zero, 4, hipMemcpyHostToDevice, st) != hipSuccess) return false;
-                        k_bfs_level<<<blocks_for(b1 - b0, kBlock), kBlock, 0, st>>>(pchild, ord + b0, b1 - b0, ord + b1, c4);
-                        if (hipMemcpyAsync(&cnt, c4, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                            hipStreamSynchronize(st) != hipSuccess)
-                            return false;
-                        off.push_back(b1 + (int)cnt);
-                    }
-                    return true;
-                };
-                int tmin = 3;  // smallest subtree (triangles) restructured
-                if (const char* e = getenv("TMPT_TREELET_MIN")) tmin = std::max(3, atoi(e));
-                std::vector<int> off;
-                for (int p = 0; p < tpass && rc == 0; ++p) {
-                    if (!bfs(off)) { rc = -1; break; }
-                    for (int L = (int)off.size() - 3; L >= 0; --L)  // deepest level first
-                        k_treelet<<<blocks_for(off[L + 1] - off[L], 64), 64, 0, st>>>(
-                            ord + off[L], off[L + 1] - off[L], pchild, leaf, vi, pib, psize, tmin, nullptr);
-                }
-                if (rc || !bfs(off)) { rc = -1; break; }
-                for (int L = 0; L + 1 < (int)off.size(); ++L)
-                    if (off[L + 1] > off[L])
-                        k_offsets_list<<<blocks_for(off[L + 1] - off[L], kBlock), kBlock, 0, st>>>(
-                            ord + off[L], off[L + 1] - off[L], pchild, psize, poff, new_slot);
-            } else {
-                for (int k = it - 1; k >= 0; --k)
-                    k_ploc_offsets<<<blocks_for(m, kBlock), kBlock, 0, st>>>(m, k, piter, pchild, psize, poff, new_slot);
-            }
+            for (int k = it - 1; k >= 0; --k)
+                k_ploc_offsets<<<blocks_for(m, kBlock), kBlock, 0, st>>>(m, k, piter, pchild, psize, poff, new_slot);
             k_ploc_relabel<<<blocks_for(m, kBlock), kBlock, 0, st>>>(m, pchild, poff, psize, prange, new_slot);
             k_ploc_vals<<<blocks_for(n, kBlock), kBlock, 0, st>>>(n, new_slot, vi, pvals);
             tchild = pchild;
@@ -1158,19 +860,15 @@ int build_lbvh(Scene& s, const float* d_tris9)
         }
         k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, tvals, s.tri_pre);
         // binary tree -> BVH4Q, top-down, one launch per level
-        int leaf_max = 2;
-        if (const char* e = getenv("TMPT_LEAF_MAX")) leaf_max = std::max(1, std::min(kLeafMaxTris, atoi(e)));
+        const int leaf_max = s.opt.leaf_max;
         s.leaf_max = leaf_max;
-        // TMPT_COLLAPSE=sah: SAH-optimal collapse (fewer, fuller nodes: 13.2k vs 16.7k
+        // collapse=1: SAH-optimal collapse (fewer, fuller nodes: 13.2k vs 16.7k
         // on the sponza stand-in, but measured ~2% slower there); default greedy
         // largest-area opening
-        const char* ce = getenv("TMPT_COLLAPSE");
-        const bool sah = ce && ce[0] == 's' && n >= 2;
+        const bool sah = s.opt.collapse == 1 && n >= 2;
         uint32_t* dec = nullptr;
         if (sah) {
-            SahCost cost{1.0f, 0.7f, 0.5f};
-            if (const char* e = getenv("TMPT_SAH_CLEAF")) cost.c_leaf = (float)atof(e);
-            if (const char* e = getenv("TMPT_SAH_CTRI")) cost.c_tri = (float)atof(e);
+            const SahCost cost{1.0f, s.opt.sah_c_leaf, s.opt.sah_c_tri};
             int32_t* ord = (int32_t*)alloc((size_t)m * 4);
             float4* Fc = (float4*)alloc((size_t)m * sizeof(float4));
             dec = (uint32_t*)alloc((size_t)m * 4);
@@ -1197,15 +895,13 @@ int build_lbvh(Scene& s, const float* d_tris9)
             hipMemcpyAsync(c4, hc, sizeof(hc), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
         int nf = 1, levels = 0;
         int2 *fa = fr0, *fb = fr1;
-        std::vector<int> lev = {0, 1};  // level l of the BVH4 = slots [lev[l], lev[l+1])
         while (nf > 0) {
             k_bvh4_level<<<blocks_for(nf, kBlock), kBlock, 0, st>>>(tchild, trange, leaf, tvals, tib, fa, nf,
-                                                                    fb, c4, s.nodes4, s.nodes4f, leaf_max, n, dec);
+                                                                    fb, c4, s.nodes4, leaf_max, n, dec);
             ++levels;
             if (hipMemcpyAsync(hc, c4, sizeof(hc), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }
             nf = (int)hc[1];
-            if (nf > 0) lev.push_back((int)hc[0]);
             hc[1] = 0;
             if (hipMemcpyAsync(c4 + 1, &hc[1], 4, hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
             std::swap(fa, fb);
@@ -1213,31 +909,6 @@ int build_lbvh(Scene& s, const float* d_tris9)
         if (rc) break;
         s.n_nodes4 = (int32_t)hc[0];
         s.depth4 = levels;
-        const char* le = getenv("TMPT_LAYOUT");
-        const int n4 = s.n_nodes4;
-        if (le && atoi(le) == 1 && n4 > kTopNodes) {
-            int32_t* desc = (int32_t*)alloc((size_t)n4 * 4);
-            int32_t* cbk = (int32_t*)alloc((size_t)n4 * 4);
-            int32_t* nidx = (int32_t*)alloc((size_t)n4 * 4);
-            Bvh4Node* o4 = (Bvh4Node*)alloc((size_t)n4 * sizeof(Bvh4Node));
-            Bvh4FNode* o4f = (Bvh4FNode*)alloc((size_t)n4 * sizeof(Bvh4FNode));
-            if (!desc || !cbk || !nidx || !o4 || !o4f) { set_error("build: out of device memory (layout)"); rc = -1; break; }
-            const int nl = (int)lev.size() - 1;
-            for (int l = nl - 1; l >= 0; --l)
-                k_desc_level<<<blocks_for(lev[l + 1] - lev[l], kBlock), kBlock, 0, st>>>(s.nodes4, lev[l], lev[l + 1], desc);
-            k_top_blocks<<<1, 1, 0, st>>>(s.nodes4, kTopNodes, desc, cbk, nidx);
-            for (int l = 0; l < nl; ++l) {
-                const int lo = std::max(lev[l], 0), hi = lev[l + 1];
-                // top nodes' blocks come from k_top_blocks; their non-top children are placed here too
-                k_place_level<<<blocks_for(hi - lo, kBlock), kBlock, 0, st>>>(s.nodes4, lo, hi, kTopNodes, desc, cbk, nidx);
-            }
-            k_relayout<<<blocks_for(n4, kBlock), kBlock, 0, st>>>(s.nodes4, s.nodes4f, n4, nidx, o4, o4f);
-            if (hipMemcpyAsync(s.nodes4, o4, (size_t)n4 * sizeof(Bvh4Node), hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(s.nodes4f, o4f, (size_t)n4 * sizeof(Bvh4FNode), hipMemcpyDeviceToDevice, st) != hipSuccess) {
-                rc = -1;
-                break;
-            }
-        }
         if (3 * levels + 1 > kStackTotal) {
             set_error("build_lbvh: BVH4 depth " + std::to_string(levels) + " exceeds the traversal stack");
             rc = -2;

@@ -1,10 +1,10 @@
 // tmpt_internal.h -- device data layout and the scene object behind the C ABI.
 //
 // HBM layout of one scene (DESIGN.md "Data layout in HBM"):
-//   nodes    BvhNode[max(n-1,1)]  64 B  LBVH2 internal nodes; each holds BOTH
-//                                        child boxes, so one node visit is one
-//                                        128-B line (4 x dwordx4 loads)
-//   tri_pre  TriPre[n]            48 B  leaf order: v0, e1 = v1-v0, e2 = v2-v0,
+//   nodes4   Bvh4Node[<= n-1]     64 B  4-wide BVH, quantised child boxes,
+//                                        numbered level by level (the top
+//                                        kTopNodes are copied to LDS)
+//   tri_pre  TriPre[n + 1]        48 B  leaf order: v0, e1 = v1-v0, e2 = v2-v0,
 //                                        original index (the Moller-Trumbore operands)
 //   tri_orig TriOrig[n]           48 B  original order: v0, v1, v2 and the geometric
 //                                        normal, read once per accepted hit
@@ -19,14 +19,6 @@
 #include "tmpt_math.h"
 
 namespace tmpt {
-
-struct alignas(16) BvhNode {
-    float4 a;  // c0.min.xyz, c0.max.x
-    float4 b;  // c0.max.yz,  c1.min.xy
-    float4 c;  // c1.min.z,   c1.max.xyz
-    int4 d;    // child0, child1 (>=0 internal node, <0 leaf = ~triangle slot), depth, 0
-};
-static_assert(sizeof(BvhNode) == 64, "node is one half cache line");
 
 // 4-wide node with quantised child boxes (DESIGN.md "BVH4Q"): 64 B, one
 // half cache line, 4 x dwordx4 loads for FOUR child boxes.
@@ -45,38 +37,10 @@ struct alignas(16) Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 64, "BVH4Q node is one half cache line");
 
-// BVH4F: the same 4-wide tree with full-precision child boxes, one 128-B line
-// per node.  Planes are grouped [axis][lo|hi][child] so a ray picks its near and
-// far plane of an axis by a byte offset (octant), not by per-child min/max; an
-// empty child slot has lo = +inf, hi = -inf and misses every ray.
-struct alignas(128) Bvh4FNode {
-    float4 p[6];  // lo_x, hi_x, lo_y, hi_y, lo_z, hi_z (child k in component k)
-    int4 links;
-    int4 pad;
-};
-static_assert(sizeof(Bvh4FNode) == 128, "BVH4F node is one 128-B line");
 constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
-constexpr int kTopNodes = 120;  // FMT 4: BVH4 nodes held in LDS per path block (7.5 KB)
-
-// Light-space grid for the shadow query (tmpt_shadow.hip): R x R cells over
-// the plane orthogonal to the light direction, per cell the triangles whose
-// projection overlaps it, sorted by how far up the light direction they reach.
-struct ShadowGrid {
-    float U[3] = {0, 0, 0}, V[3] = {0, 0, 0};  // plane axes (L = light_dir())
-    float u0 = 0, v0 = 0, inv_cu = 0, inv_cv = 0;
-    int R = 0;                  // 0: no grid
-    uint32_t* start = nullptr;  // R*R + 1 entry offsets, cell = iv * R + iu
-    float* tmax = nullptr;      // per entry: max over the triangle's vertices of dot(v, L), rounded up
-    uint32_t* slot = nullptr;   // per entry: tri_pre slot
-    int64_t n_entries = 0;
-    // the path kernel's form: each entry's TriPre copied into tri_pre after the
-    // scene's slots (from index base), so a cell's list is one contiguous range
-    // that the traversal's leaf step tests like any leaf
-    uint2* cell = nullptr;      // per cell: {first tri_pre index, count}
-    int32_t base = 0;
-};
+constexpr int kTopNodes = 120;  // BVH4 nodes held in LDS per path block (7.5 KB)
 
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x
@@ -97,26 +61,53 @@ constexpr float kBoxPadRel = 1e-5f;
 constexpr float kTfarSlack = 1.00001f;
 
 // Stack: SL entries per lane live in LDS, the rest spill to a global per-lane
-// area.  BVH2: depth <= 62 for (30-bit Morton, index) keys, <= depth+1 entries;
-// BVH4Q: <= 3 per level.  The build rejects trees that could exceed
-// kStackTotal (DESIGN.md "Traversal").
+// area.  BVH4Q: <= 3 entries per level.  The build rejects trees that could
+// exceed kStackTotal (DESIGN.md "Traversal").
 constexpr int kStackTotal = 128;
 
 constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
 
+// Per-scene options: the library's control plane in place of environment
+// variables (include/tmpt.h documents each key).  Build options are fixed when
+// the scene is created; render options apply to the renders after they are set.
+struct Options {
+    // build (tmpt_scene_create_ex)
+    int builder = 0;      // 0 = PLOC (Meister & Bittner 2018), 1 = LBVH (Karras 2012)
+    int leaf_max = 2;     // triangles per BVH4 leaf, 1..kLeafMaxTris
+    int collapse = 0;     // BVH2 -> BVH4: 0 = greedy largest-area opening, 1 = SAH-optimal
+    int ploc_radius = 32; // PLOC nearest-neighbour search radius
+    float sah_c_leaf = 0.7f, sah_c_tri = 0.5f;  // SAH collapse costs (inner node = 1)
+    // render (tmpt_scene_set_option)
+    int sample_block = 0;     // sample seeding: samples per work unit, a power of two (0 = auto)
+    double sbuf_max = 0.0;    // sample seeding: cap on the per-sample colour buffer, bytes (0 = 3/4 of free HBM)
+    int pilot = -1;           // pixel seeding: pilot-pass samples of the cost ordering (-1 auto, 0 off)
+    int help = -1;            // pixel seeding: shadow offload to idle lanes (-1 auto, 0 off, 1 on)
+    int pair = -1;            // pixel seeding: expensive ranks per 64-rank chunk with offload (-1 auto)
+    int balance = 1;          // pixel seeding: SIMD-balanced first chunks
+    int dprio = 1;            // pixel seeding: longest-remaining-first wave priority with offload
+    int wave_cap = 0;         // pixel seeding: pixels a wave holds at once (0 auto, else 1..64)
+    int rowspec = 1;          // row seeding: speculative row engine (0 = one lane per row chain)
+    int rowspec_wmax = 0;     // row seeding: units per window (0 = auto: 24 x spp)
+    int rowspec_windows = 0;  // row seeding: windows per row and iteration (0 = auto)
+    float rowspec_spread = -1.0f;  // row seeding: window spread in pixels (-1 = auto)
+    int rowspec_groups = 2;   // row seeding: row groups on their own streams
+    int rowspec_noshadow = 1; // row seeding: shadow-free speculation + one full re-trace of the chain
+};
+int options_parse(Options& o, const char* text, bool allow_build);
+int options_set(Options& o, const char* key, double value, bool allow_build);
+int options_get(const Options& o, const char* key, double* value);
+
 struct Scene {
     int device = 0;
     int32_t n = 0;          // triangles incl. the floor
-    int32_t n_nodes = 0;    // internal nodes
-    int32_t max_depth = 0;  // of the LBVH
-    BvhNode* nodes = nullptr;
+    int32_t n_nodes = 0;    // internal nodes of the binary tree the BVH4 is collapsed from
+    int32_t max_depth = 0;  // of the LBVH (Karras builder)
     Bvh4Node* nodes4 = nullptr;
-    Bvh4FNode* nodes4f = nullptr;  // same tree, f32 child boxes
     int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
-    bool has_bvh2 = true;  // the LBVH2 (A/B layout) matches tri_pre only for the LBVH builder
     TriPre* tri_pre = nullptr;
-    ShadowGrid sgrid;  // shadow-query grid (tmpt_shadow.hip), R = 0 if none
     TriOrig* tri_orig = nullptr;
+    Options opt;  // build and render options (tmpt_scene_create_ex / tmpt_scene_set_option)
+    hipEvent_t wait_ev = nullptr;  // TMPT_FLAG_WAIT_STREAM: reused across renders
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
     // render workspace (grown on demand, reused across calls)
@@ -179,9 +170,6 @@ void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab);
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tkeys, uint32_t* tvals, int32_t n,
                      int bits, uint32_t* hist, hipStream_t st);
 size_t radix_sort_hist_words(int32_t n);
-// shadow-query grid (tmpt_shadow.hip); host_tris = the n x 9 input floats
-int build_shadow_grid(Scene& s, const float* host_tris);
-void free_shadow_grid(Scene& s);
 
 TMPT_HD float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 

@@ -110,27 +110,16 @@ __device__ __forceinline__ void flush_counts(unsigned long long* counters, uint3
 }
 
 // ============================================================ megakernel
-// Whole query; Q2: the persistent engine's step (octant decode, top nodes from
-// the block's LDS copy), for the latency-bound row chains.
-template <bool WIDE, bool ANY, bool COUNT, bool Q2, int BLOCK, int SL>
+// Whole query; TOPC: the top BVH4 levels from the block's LDS copy (the
+// latency-bound row chains).
+template <bool ANY, bool COUNT, bool TOPC, int BLOCK, int SL>
 __device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float& t, float& u, float& v,
                                           TravStack<BLOCK, SL>& st, TravCount& cnt)
 {
-    if (!Q2) return traverse<WIDE, ANY, COUNT>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
-    TravState ts;
-    trav_init(ts, kMaxT);
-    if (sv.n > 0 && !ray_has_nan(o, d)) {
-        const TravRay r = make_trav_ray(o, d);
-        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, 1, true>(sv, r, ANY, ts, st, cnt)) {
-        }
-    }
-    t = ts.bt;
-    u = ts.bu;
-    v = ts.bv;
-    return ts.best;
+    return traverse<ANY, COUNT, BLOCK, SL, TOPC>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
 }
 
-template <bool WIDE, bool COUNT, int BLOCK, int SL, bool Q2 = false>
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
                                          TravCount& cnt)
@@ -140,7 +129,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
         ++rays;
         float t, u, v;
-        int id = mega_query<WIDE, false, COUNT, Q2>(sv, o, d, t, u, v, st, cnt);
+        int id = mega_query<false, COUNT, TOPC>(sv, o, d, t, u, v, st, cnt);
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
@@ -148,7 +137,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
             float lc = light_cosine(nrm, d);
             if (lc > 0.0f) {  // a zero light term does not depend on the answer
                 float ts, us, vs;
-                int sid = mega_query<WIDE, true, COUNT, Q2>(sv, pos, light_dir(), ts, us, vs, st, cnt);
+                int sid = mega_query<true, COUNT, TOPC>(sv, pos, light_dir(), ts, us, vs, st, cnt);
                 if (sid >= 0) lc = 0.0f;
             }
             lbuf[depth * BLOCK] = lc;
@@ -166,7 +155,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
     return color;
 }
 
-template <bool WIDE, bool COUNT, int BLOCK, int SL, bool Q2 = false>
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false>
 __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const RenderArgs& a, int x,
                                                  int y, uint32_t& rng, uint32_t& rays,
                                                  TravStack<BLOCK, SL>& st, float* lbuf,
@@ -178,12 +167,12 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
         f3 o, d;
         if (a.jt) rng = sample_seed(a.jt, (uint32_t)s, pseed);  // sample seeding
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-        col = col + trace_path<WIDE, COUNT, BLOCK, SL, Q2>(sv, o, d, rng, rays, st, lbuf, cnt);
+        col = col + trace_path<COUNT, BLOCK, SL, TOPC>(sv, o, d, rng, rays, st, lbuf, cnt);
     }
     return pack_pixel(col, a.spp_recip);
 }
 
-template <bool WIDE, bool ROW, bool COUNT, int BLOCK, int SL>
+template <bool ROW, bool COUNT, int BLOCK, int SL>
 __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -196,9 +185,9 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
     float* lbuf = &s_light[threadIdx.x];
     // ROW (one latency-bound chain per wave): the persistent engine's node step,
     // with the top BVH4 levels copied to LDS
-    constexpr bool Q2 = ROW && WIDE;
-    if (Q2) {
-        __shared__ uint4 s_top[Q2 ? kTopNodes * 4 : 1];
+    constexpr bool TOPC = ROW;
+    if (TOPC) {
+        __shared__ uint4 s_top[TOPC ? kTopNodes * 4 : 1];
         const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
         const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
         for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
@@ -219,19 +208,23 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
             int y = tile_row_to_y(a, lr);
             uint32_t rng = row_seed((uint32_t)y);  // main.cpp:204, unmodified
             for (int x = 0; x < a.W; ++x)
-                out[(int64_t)lr * a.W + x] = render_pixel<WIDE, COUNT, BLOCK, SL, Q2>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+                out[(int64_t)lr * a.W + x] = render_pixel<COUNT, BLOCK, SL, TOPC>(sv, a, x, y, rng, rays, st, lbuf, cnt);
         } else {
             int lr = (int)(w / a.W), x = (int)(w - (int64_t)lr * a.W);
             int y = tile_row_to_y(a, lr);
             uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)a.W);
-            out[w] = render_pixel<WIDE, COUNT>(sv, a, x, y, rng, rays, st, lbuf, cnt);
+            out[w] = render_pixel<COUNT, BLOCK, SL, TOPC>(sv, a, x, y, rng, rays, st, lbuf, cnt);
         }
     }
     flush_counts<BLOCK, COUNT>(counters, rays, cnt);
 }
 
 // ============================================================ batched HitScene
-template <bool WIDE, bool ANY, int BLOCK, int SL>
+// Scene::HitScene (scene.cpp:129-140) over a batch: rays n x {o.xyz, d.xyz}
+// with one [tmin, tmax] for all (RANGED = 0), or n x {o.xyz, d.xyz, tmin, tmax}
+// (RANGED = 1, the per-call range of scene.h:36-37).  hits n x {pos, normal, t}
+// where ids >= 0.
+template <bool ANY, bool RANGED, int BLOCK, int SL>
 __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* __restrict__ rays,
                                                      int64_t n, float tmin, float tmax,
                                                      float* __restrict__ hits,
@@ -242,17 +235,13 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     TravCount cnt;
+    constexpr int kStride = RANGED ? 8 : 6;
     for (int64_t i = gtid; i < n; i += (int64_t)gridDim.x * BLOCK) {
-        const float* r = rays + 6 * i;
+        const float* r = rays + kStride * i;
         f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+        const float t0 = RANGED ? r[6] : tmin, t1 = RANGED ? r[7] : tmax;
         float t, u, v;
-        const f3 ld = light_dir();
-        int id;
-        if (ANY && sv.sg.R > 0 && tmin == kMinT && tmax == kMaxT && d.x == ld.x && d.y == ld.y &&
-            d.z == ld.z && !ray_has_nan(o, d) && sv.n > 0)
-            id = shadow_grid_hit(sv, o, d, t, u, v);  // the shadow query's own structure
-        else
-            id = traverse<WIDE, ANY, false>(sv, make_trav_ray(o, d), tmin, tmax, t, u, v, st, cnt);
+        const int id = traverse<ANY, false, BLOCK, SL>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
         ids[i] = id;
         if (id >= 0) {
             f3 pos, nrm;
@@ -336,10 +325,10 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 // reservation is renewed by ONE atomic on the head of the wave's current
 // segment; exhausted segments are skipped, starting from the wave's own, so
 // waves work on nearby pixels and the heads see few atomics.  Lanes run
-// STEPS traversal steps between refill checks.
-template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 8, int MINW = 1,
-          int PROBE = 0, int SORT = !ANY, int VOTE = 1>
-__global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState s, int parity,
+// STEPS traversal steps between refill checks, each step of the kind (node or
+// leaf) more lanes are waiting for.
+template <bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 8>
+__global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int parity,
                                                     uint32_t* __restrict__ ovf)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
@@ -355,7 +344,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     const uint32_t wave_gid = (uint32_t)(gtid >> 6);
     uint32_t seg = wave_gid % kSeg;  // current segment; starts spread over the frame
-    bool probe = false, drained = false;
+    bool drained = false;
     uint32_t walked = 0;
     uint32_t res = 0, res_end = 0;          // reservation [res, res_end) of queue positions
     bool active = false;
@@ -368,22 +357,6 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
         uint32_t nidle = (uint32_t)__popcll(idle);
         if (nidle >= (uint32_t)REFILL && (res < res_end || !drained)) {
             while (res >= res_end && !drained) {  // renew the reservation (wave-uniform)
-                if (probe) {
-                    // the current segment ran dry: lane j probes segment j, so ONE round
-                    // trip finds every segment with entries left (or proves the queue empty)
-                    const uint32_t cj = counts[lane_id() * kCtr];
-                    const uint32_t hj = __hip_atomic_load(&heads[lane_id() * kCtr], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t open = wballot(hj < cj);
-                    if (open == 0) {
-                        drained = true;
-                        break;
-                    }
-                    // first open segment after the current one (rotate the mask)
-                    const uint64_t rot = (open >> seg) | (seg ? (open << (64 - seg)) : 0ull);
-                    seg = (seg + (uint32_t)(__ffsll((unsigned long long)rot) - 1)) & 63u;
-                    probe = false;
-                }
                 const uint32_t c = counts[seg * kCtr];
                 uint32_t b = 0;
                 if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
@@ -391,8 +364,6 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                 if (b < c) {
                     res = seg * s.seg_cap + b;
                     res_end = seg * s.seg_cap + min(b + kChunk, c);
-                } else if (PROBE) {
-                    probe = true;
                 } else {  // sequential walk: try the next segment, give up after all 64
                     seg = (seg + 1) & 63u;
                     if (++walked == kSeg) drained = true;
@@ -432,23 +403,15 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
         if (active) {
             bool done = false;
             for (int k = 0; k < STEPS; ++k) {
-                if (VOTE) {
-                    // one step kind per round: inner nodes or leaves, whichever more
-                    // lanes are waiting for, so each load issues with more lanes
-                    const uint64_t at_leaf = wballot(!done && ts.node < 0);
-                    const uint64_t at_node = wballot(!done && ts.node >= 0);
-                    if (at_leaf == 0 && at_node == 0) break;
-                    const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
-                    if (!done && (ts.node < 0) == leaf_round) {
-                        done = trav_step_w<WIDE, ANY, COUNT, BLOCK, SL, (bool)SORT>(sv, r, 0.0f, kMinT, kMaxT, ts,
-                                                                                 st, cnt);
-                        if (COUNT) ++steps;
-                    }
-                } else {
-                    done = trav_step_w<WIDE, ANY, COUNT, BLOCK, SL, (bool)SORT>(sv, r, 0.0f, kMinT, kMaxT, ts, st,
-                                                                             cnt);
+                // one step kind per round: inner nodes or leaves, whichever more
+                // lanes are waiting for, so each load issues with more lanes
+                const uint64_t at_leaf = wballot(!done && ts.node < 0);
+                const uint64_t at_node = wballot(!done && ts.node >= 0);
+                if (at_leaf == 0 && at_node == 0) break;
+                const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
+                if (!done && (ts.node < 0) == leaf_round) {
+                    done = trav_step4q2_mixed<COUNT, BLOCK, SL>(sv, r, ANY, ts, st, cnt);
                     if (COUNT) ++steps;
-                    if (done) break;
                 }
             }
             if (done) {
@@ -608,10 +571,8 @@ struct PathCtl {
     uint32_t* claim;  // nchunks words, zeroed per launch
     uint32_t nsimd, wps;
     int64_t P;
-    int cost_map;                     // COUNT only: write per-pixel traversal work instead of colour
     const uint32_t* __restrict__ order;  // rank -> pixel, or null
     uint32_t* __restrict__ cost_out;     // per-pixel traversal steps of this call, or null
-    uint32_t prio_q;  // ordered pass: ranks per wave-priority level (s_setprio 3..0), 0 = off
     // dynamic issue priority (longest remaining first): each shading round the
     // wave estimates its lanes' remaining traversal steps (steps so far per
     // finished sample x samples left) and sets s_setprio 3/2/1/0 at the
@@ -620,18 +581,15 @@ struct PathCtl {
     // fractions of the heaviest pixel's (order[0]) projected remaining steps.
     float dprio[3];
     const uint32_t* __restrict__ dprio_cost;
-    int diag_noshadow;  // diagnostic (TMPT_DIAG_NOSHADOW=1, wrong images): shadow queries answered "clear" untraced
     uint32_t lane_cap;  // pixels a wave holds at once (64: all lanes)
     uint32_t chunk;     // ranks per chunk (kChunk, or lane_cap when capped)
-    uint32_t* __restrict__ tlog;  // PROF: per pixel {start, end (s_memrealtime), steps, shading rounds}
     // Sample seeding: the supply hands out units = (pixel, block of blk
     // samples), nblk blocks per pixel, unit u = pixel * nblk + block (P counts
     // units).  With nblk > 1 each sample's colour goes to sbuf[s * slots + pixel]
     // and k_resolve sums them in sample order (main.cpp:218's col += Trace).
     uint32_t nblk, blk;
     float4* __restrict__ sbuf;
-    uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp
-    int sb_nt;              // nontemporal stores
+    uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp ([pixel][sample]: 1, spp)
     // Speculative row seeding (SAMP 2, render_rowspec): unit u traces ONE
     // sample of tile pixel upix[u] from RNG state ustate[u] and writes its
     // colour with w = draws | rays << 27 to rs_out[u], and its final RNG state
@@ -641,16 +599,12 @@ struct PathCtl {
     float4* __restrict__ rs_out;
     uint32_t* __restrict__ rs_end;
     const uint32_t* __restrict__ p_dev;  // the unit count (replaces P, nchunks at launch)
-    // no-shadow speculation (TMPT_ROWSPEC_NOSHADOW): the speculative pass skips
+    // no-shadow speculation (option rowspec_noshadow): the speculative pass skips
     // shadow traversals (they never change a sample's draws); the chain's
     // samples are traced again in full at the end of the frame, unit u as
     // sample uslot[u] of its pixel, colour into sbuf (resolved in order)
     int rs_noshadow;
     const uint32_t* __restrict__ uslot;
-    // sample kernel at 5 waves per SIMD (OCC 5, A/B): light terms and the
-    // pending scattered ray per lane in global memory, [k][lane] (LDS holds
-    // only the stack and the top nodes)
-    float* __restrict__ gl_store;
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -684,8 +638,8 @@ __device__ __forceinline__ uint2 simd_rank(uint32_t* reg)
 }
 
 
-template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int VOTE = 1, int FMT = 1,
-          int OCC = 1, int TAIL = 0, int PROF = 0, int HELP = 0, int SAMP = 0>
+template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int OCC = 1, int TAIL = 0, int PROF = 0,
+          int HELP = 0, int SAMP = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -693,17 +647,16 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
     // SAMP 3 (shadow-free speculation): no light terms, no pending next ray
-    constexpr bool kGL = SAMP == 1 && OCC >= 5;
-    __shared__ float s_light[(SAMP == 3 || kGL) ? 1 : kMaxDepth * BLOCK];
-    __shared__ float s_next[(SAMP == 3 || kGL) ? 1 : 6 * BLOCK];
+    __shared__ float s_light[SAMP == 3 ? 1 : kMaxDepth * BLOCK];
+    __shared__ float s_next[SAMP == 3 ? 1 : 6 * BLOCK];
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
-    const uint32_t LS = kGL ? gridDim.x * BLOCK : BLOCK;  // stride between a lane's entries
-    float* light = kGL ? pc.gl_store + gtid : &s_light[threadIdx.x];
-    float* nxt = kGL ? pc.gl_store + (size_t)kMaxDepth * LS + gtid : &s_next[threadIdx.x];
+    constexpr uint32_t LS = BLOCK;  // stride between a lane's LDS entries
+    float* light = &s_light[threadIdx.x];
+    float* nxt = &s_next[threadIdx.x];
     // HELP: lane ids of this round's offloading lanes, by rank (per wave)
     __shared__ uint8_t s_pair[HELP ? BLOCK : 1];
-    if (FMT == 4) {  // the top BVH4 levels (nodes are numbered level by level) in LDS
+    {  // the top BVH4 levels (nodes are numbered level by level) in LDS
         // HELP: 4 nodes fewer, so s_pair keeps the block at 4 per CU
         constexpr int kTop = HELP ? kTopNodes - 4 : kTopNodes;
         __shared__ uint4 s_top[kTop * 4];
@@ -715,9 +668,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         st.ntop = ntop;
     }
     // SAMP: the sample kernel has none of pixel mode's pilot order, balanced
-    // first chunks, priorities, progressive state, trace log or shadow grid
-    // (answers without the grid are the same); compiling them out frees the
-    // scalar registers they held
+    // first chunks, priorities or progressive state; compiling them out frees
+    // the scalar registers they held
     constexpr bool kFull = !SAMP;
     float dp0 = kFull ? pc.dprio[0] : 0.0f, dp1 = kFull ? pc.dprio[1] : 0.0f, dp2 = kFull ? pc.dprio[2] : 0.0f;
     if (kFull && pc.dprio_cost && pc.order && a.smp_begin > 0) {  // relative thresholds (wave-uniform)
@@ -776,9 +728,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf_smp = 0xFFFFFFFFu, pf_pix = 0;
     // SAMP 2: the unit held, the ray counts at its start, the camera's RNG draws
     uint32_t cur_unit = 0, re0 = 0, rs0 = 0, ndraw = 0;
-    uint32_t work0 = 0;  // COUNT + cost map: traversal work at the pixel's start
     uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
-    uint32_t pt0 = 0, pnsh = 0;  // PROF + tlog: pixel start time, shading rounds while held
     // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
     // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
     uint64_t rs_nr = 0, rs_nl = 0, rs_lr = 0, rs_ll = 0, rs_sr = 0, rs_sl = 0, rs_st = 0;
@@ -805,7 +755,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             shade_min = max(1, min(SHADE_MIN, act / TAIL));
         }
         if (need != 0 && (__popcll(need) >= shade_min || trav == 0)) {
-            if (PROF && has_pix) ++pnsh;
             if (COUNT || PROF >= 3) {
                 ++rs_sr;
                 rs_sl += (uint64_t)__popcll(need);
@@ -816,7 +765,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             // branches, so the wave runs each at most once per round.
             bool cam = false, start = false, sany = false;
             f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
-            uint2 gcell = make_uint2(0u, 0u);  // shadow-grid leaf range of this round's shadow query
             // ---- new pixels for idle lanes (wave-uniform reservation)
             const uint64_t nopix = wballot(!has_pix && !(HELP && helper) && !exhausted);
             if (nopix != 0) {
@@ -836,13 +784,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (b < c) {
                         res = (seg + b * (uint32_t)kSeg) * pc.chunk;
                         res_end = (uint32_t)min<int64_t>((int64_t)res + pc.chunk, pc.P);
-                        if (kFull && pc.prio_q != 0) {  // issue priority by cost rank (wave-uniform)
-                            const uint32_t q = res / pc.prio_q;
-                            if (q == 0) __builtin_amdgcn_s_setprio(3);
-                            else if (q == 1) __builtin_amdgcn_s_setprio(2);
-                            else if (q == 2) __builtin_amdgcn_s_setprio(1);
-                            else __builtin_amdgcn_s_setprio(0);
-                        }
                     } else {
                         seg = (seg + 1) & 63u;
                         if (++walked == kSeg) exhausted = true;
@@ -868,11 +809,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         pix = (kFull && pc.order) ? pc.order[res + k] : res + k;
                     }
                     psteps = 0;
-                    if (PROF && kFull && pc.tlog) {
-                        pt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                        pnsh = 0;
-                    }
-                    if (!PROF && kFull && pc.tlog) pc.tlog[4 * (size_t)pix] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
@@ -888,8 +824,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     }
                     smp = smp0;
                     depth = 0;
-                    if (COUNT) work0 = pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
-                                                        : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris;
                     cam = true;
                 }
                 res += take;
@@ -930,25 +864,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
-                        bool traced = false;
-                        if (SAMP != 3 && lc > 0.0f && !(kFull && pc.diag_noshadow) && !(SAMP == 2 && pc.rs_noshadow)) {
-                            // shadow query: with the light-space grid, the triangles of
-                            // the origin's cell (one leaf range, tested by the leaf
-                            // steps of the traversal rounds); without, the BVH
-                            const bool grid = kFull && sv.sg.R > 0;
-                            if (grid) gcell = shadow_grid_cell(sv, pos);
-                            if (!grid || gcell.y != 0) {
-                                nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
-                                nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
-                                start = true;  // shadow query toward the light
-                                sany = true;
-                                so = pos;
-                                sd = ldir;
-                                traced = true;
-                                want_off = HELP != 0 && !grid;
-                            }
-                        }
-                        if (!traced) {  // nothing to trace (no light term, or an empty cell)
+                        if (SAMP != 3 && lc > 0.0f && !(SAMP == 2 && pc.rs_noshadow)) {
+                            nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
+                            nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
+                            start = true;  // shadow query toward the light
+                            sany = true;
+                            so = pos;
+                            sd = ldir;
+                            want_off = HELP != 0;
+                        } else {  // nothing to trace (no light term)
                             // The reference still calls HitScene for the shadow ray
                             // (main.cpp:57, counted), but a surface turned away from
                             // the light adds max(0, cos) = 0 whatever it answers
@@ -1036,15 +960,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             make_float4(SAMP == 3 ? 0.0f : color.x, SAMP == 3 ? 0.0f : color.y, SAMP == 3 ? 0.0f : color.z,
                                         __uint_as_float(draws | (nr << 23) | (ne << 28)));
                         pc.rs_end[cur_unit] = rng;
-                    } else if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve sums in sample order
-                        float4* dst = pc.sbuf + ((size_t)smp * pc.sb_ss + (size_t)pix * pc.sb_sp);
-                        const float4 v = make_float4(color.x, color.y, color.z, 0.0f);
-                        if (pc.sb_nt) {
-                            typedef float f32x4 __attribute__((ext_vector_type(4)));
-                            __builtin_nontemporal_store((f32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(dst));
-                        } else {
-                            *dst = v;
-                        }
+                    } else if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve_px sums in sample order
+                        typedef float f32x4 __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
+                                                    reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss +
+                                                                                        (size_t)pix * pc.sb_sp)));
                     } else
                         col = col + color;
                     ++smp;
@@ -1054,22 +974,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     } else {
                         if (kFull && a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
                         if (kFull && pc.cost_out) pc.cost_out[pix] = psteps;
-                        if (PROF && kFull && pc.tlog)
-                            *reinterpret_cast<uint4*>(&pc.tlog[4 * (size_t)pix]) =
-                                make_uint4(pt0, (uint32_t)__builtin_amdgcn_s_memrealtime(), psteps, pnsh);
-                        if (!PROF && kFull && pc.tlog) {  // start was stored at the fetch
-                            pc.tlog[4 * (size_t)pix + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                            pc.tlog[4 * (size_t)pix + 2] = psteps;
-                            // where it ran: XCC_ID << 16 | HW_ID[15:0] (wave, SIMD, CU, SH, SE)
-                            pc.tlog[4 * (size_t)pix + 3] = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) |
-                                                           (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu);
-                        }
-                        if (SAMP < 2 && (!SAMP || !pc.sbuf))
-                            out[pix] = (COUNT && pc.cost_map)
-                                           ? (pc.cost_map == 2 ? cnt_s.nodes + cnt_s.tris
-                                                               : cnt.nodes + cnt.tris + cnt_s.nodes + cnt_s.tris) -
-                                                 work0
-                                           : pack_pixel(col, a.out_recip);
+                        if (SAMP < 2 && (!SAMP || !pc.sbuf)) out[pix] = pack_pixel(col, a.out_recip);
                         has_pix = false;
                     }
                 }
@@ -1116,14 +1021,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
-                if (gcell.y != 0) {  // grid shadow query: its cell's list as chunks of leaf ranges
-                    const uint32_t n0 = min(gcell.y, (uint32_t)kLeafMaxTris);
-                    for (uint32_t f = gcell.x + n0; f < gcell.x + gcell.y; f += kLeafMaxTris)
-                        st.push(ts.sp, (int)(0x80000000u |
-                                             ((min((uint32_t)kLeafMaxTris, gcell.x + gcell.y - f) - 1u)
-                                              << kLeafCountShift) | f));
-                    ts.node = (int)(0x80000000u | ((n0 - 1u) << kLeafCountShift) | gcell.x);
-                }
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
         }
@@ -1163,40 +1060,33 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             const uint32_t n_node = (uint32_t)__builtin_popcount((uint32_t)at_node) +
                                     (uint32_t)__builtin_popcount((uint32_t)(at_node >> 32));
             const bool leaf_round = n_leaf > n_node;
-            // VOTE 2: vote only while the wave is busy; a sparse wave runs both kinds
-            // (latency of the few remaining pixels over lane efficiency)
-            const bool vote = VOTE == 1 || (VOTE == 2 && __popcll(at_leaf | at_node) >= 16);
             if (COUNT || PROF >= 3) {
-                if (!vote || !leaf_round) { ++rs_nr; rs_nl += (uint64_t)__popcll(at_node); }
-                if (!vote || leaf_round) { ++rs_lr; rs_ll += (uint64_t)__popcll(at_leaf); }
+                if (!leaf_round) { ++rs_nr; rs_nl += (uint64_t)__popcll(at_node); }
+                if (leaf_round) { ++rs_lr; rs_ll += (uint64_t)__popcll(at_leaf); }
             }
-            if (FMT == 4 && !COUNT && vote) {
+            if (!COUNT) {
                 // voted round: the kind is wave-uniform, so only its code runs
                 // (a scalar branch instead of exec-mask splits around both)
                 const bool stepping = in_query && ((ts.node < 0) == leaf_round);
                 bool done = false;
                 if (leaf_round) {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, 1, true, 2>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2>(sv, r, qany, ts, st, cnt);
                 } else {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, 1, true, 1>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1>(sv, r, qany, ts, st, cnt);
                 }
                 if (done) in_query = false;
-                if (stepping && ((kFull && (pc.cost_out || pc.tlog)) || dp0 > 0.0f)) ++psteps;
-            } else if (in_query && (!vote || (ts.node < 0) == leaf_round)) {
-                if (COUNT) {
-                    TravCount c1;
-                    if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, c1)) in_query = false;
-                    TravCount& dst = qany ? cnt_s : cnt;
-                    dst.nodes += c1.nodes;
-                    dst.tris += c1.tris;
-                } else if (trav_step_fmt<FMT, COUNT>(sv, r, qany, ts, st, cnt)) {
-                    in_query = false;
-                }
-                if ((kFull && (pc.cost_out || pc.tlog)) || dp0 > 0.0f) ++psteps;
+                if (stepping && ((kFull && pc.cost_out) || dp0 > 0.0f)) ++psteps;
+            } else if (in_query && (ts.node < 0) == leaf_round) {
+                TravCount c1;
+                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true>(sv, r, qany, ts, st, c1)) in_query = false;
+                TravCount& dst = qany ? cnt_s : cnt;
+                dst.nodes += c1.nodes;
+                dst.tris += c1.tris;
+                if ((kFull && pc.cost_out) || dp0 > 0.0f) ++psteps;
             }
             if (PROF) {
                 const uint64_t t = stamp();
-                (leaf_round && vote ? pt_leaf : pt_node) += t - pt_t;
+                (leaf_round ? pt_leaf : pt_node) += t - pt_t;
                 pt_t = t;
             }
         }
@@ -1277,24 +1167,9 @@ __global__ void __launch_bounds__(256) k_order_keys(const uint32_t* __restrict__
 
 // Sample seeding with several blocks per pixel: the pixel's colour is the sum
 // of its samples' colours in sample order (main.cpp:209-219, col += Trace),
-// then main.cpp:221-233.  sbuf is [sample][pixel]: coalesced reads.
-__global__ void __launch_bounds__(256) k_resolve(const float4* __restrict__ sbuf, int64_t P, int32_t spp,
-                                                  uint32_t ss, uint32_t sp, float spp_recip,
-                                                  uint32_t* __restrict__ out)
-{
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= P) return;
-    f3 col = mk(0.0f, 0.0f, 0.0f);
-    for (int32_t s = 0; s < spp; ++s) {
-        const float4 c = sbuf[(size_t)s * ss + (size_t)p * sp];
-        col = col + mk(c.x, c.y, c.z);
-    }
-    out[p] = pack_pixel(col, spp_recip);
-}
-
-// The same over a [pixel][sample] buffer: one wave per 64 pixels stages 16
-// samples of each in LDS with coalesced 256-B reads (16 lanes per pixel run),
-// then every lane sums its own pixel's samples in order.
+// then main.cpp:221-233.  The buffer is [pixel][sample]: one wave per 64
+// pixels stages 16 samples of each in LDS with coalesced 256-B reads (16
+// lanes per pixel run), then every lane sums its own pixel's samples in order.
 __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sbuf, int64_t P, int32_t spp,
                                                     float spp_recip, uint32_t* __restrict__ out)
 {
@@ -1347,9 +1222,7 @@ struct RowSpec {
     uint32_t* total;  // units of this iteration
     unsigned long long* planned;  // units over all iterations (diagnostic)
     uint32_t wmax;
-    float margin;
-    float look_lo;  // lookahead window start, as a fraction of the pixel's expected start
-    float spread;   // > 0: windows from expected positions +- spread * sqrt(i) pixels (default)
+    float spread;   // windows from expected positions +- spread * sqrt(i) pixels
     int nwin;       // windows per row (1 = no lookahead)
     // no-shadow speculation: the chase lists the chain's samples (tile pixel,
     // start state, sample index) for the full re-trace; scratch holds a row's
@@ -1372,12 +1245,13 @@ __global__ void __launch_bounds__(256) k_rs_init(RenderArgs a, RowSpec rs)
     rs.col[r] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
-// Windows per row.  Window 0: the remaining samples of its pixel at the
-// larger of this pixel's and the previous pixel's mean draws per sample, x
-// margin, over 2 (even offsets only).  Lookahead window i: pixel x + i, from
-// look_lo of its expected start to one pixel's window past window i-1's end
-// (so the pixel can finish there if it starts anywhere in window i-1).
-// Exclusive scan into offs; total units.  One block.
+// Windows per row.  E = a pixel's expected units (spp x mean draws per
+// sample / 2: even offsets only), the mean the larger of this pixel's so far
+// and the previous pixel's.  Pixel x + i is expected to start c_i = e0 +
+// (i - 1) E units ahead (e0 = this pixel's expected rest) and end c_i + E,
+// each give or take spread * sqrt(i) * E; window i spans its start's and its
+// end's ranges (window 0 starts at 0).  Exclusive scan into offs; total units.
+// One block.
 __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
 {
     __shared__ uint32_t part[1024];
@@ -1399,21 +1273,11 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
         for (int i = 0; i < rs.nwin; ++i) {
             uint32_t w = 0, s = 0;
             if (x + (uint32_t)i < (uint32_t)a.W) {
-                if (rs.spread > 0.0f) {
-                    // pixel x + i starts near c_i = e0 + (i-1) E, give or take
-                    // spread * sqrt(i) * E; window i spans its start's and its
-                    // end's ranges
-                    const float ci = i == 0 ? 0.0f : e0 + (float)(i - 1) * E;
-                    const float ui = i == 0 ? 0.0f : rs.spread * sqrtf((float)i) * E;
-                    const float ce = e0 + (float)i * E, ue = rs.spread * sqrtf((float)(i + 1)) * E;
-                    s = i == 0 ? 0u : min(t, (uint32_t)fmaxf(0.0f, ci - ui));
-                    w = min(rs.wmax, (uint32_t)(ce + ue) + 2u - min(s, (uint32_t)(ce + ue)));
-                } else if (i == 0) {
-                    w = min(rs.wmax, (uint32_t)(e0 * rs.margin) + 2u);
-                } else {
-                    s = min(t, (uint32_t)((e0 + (float)(i - 1) * E) * rs.look_lo));
-                    w = min(rs.wmax, (t - s) + (uint32_t)(E * rs.margin) + 2u);
-                }
+                const float ci = i == 0 ? 0.0f : e0 + (float)(i - 1) * E;
+                const float ui = i == 0 ? 0.0f : rs.spread * sqrtf((float)i) * E;
+                const float ce = e0 + (float)i * E, ue = rs.spread * sqrtf((float)(i + 1)) * E;
+                s = i == 0 ? 0u : min(t, (uint32_t)fmaxf(0.0f, ci - ui));
+                w = min(rs.wmax, (uint32_t)(ce + ue) + 2u - min(s, (uint32_t)(ce + ue)));
                 t = s + w;
             }
             rs.win[i * rows + r] = w;
@@ -1579,14 +1443,7 @@ int ensure_ws(Scene& s, size_t bytes)
     return 0;
 }
 
-SceneView view(const Scene& s)
-{
-    SceneView v{s.nodes, s.nodes4, reinterpret_cast<const char*>(s.nodes4f), s.tri_pre,
-                s.tri_orig, s.n, s.sgrid, s.n_nodes4};
-    const char* e = getenv("TMPT_SHADOW_GRID");  // 0: keep the grid out of the queries (A/B)
-    if (e && atoi(e) == 0) v.sg.R = 0;
-    return v;
-}
+SceneView view(const Scene& s) { return SceneView{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4}; }
 
 // Columns of M^n, M the xorshift32 step as a GF(2) 32x32 matrix (maths.cpp:5-13):
 // column j = image of bit j.
@@ -1669,14 +1526,14 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     a.jt = nullptr;
     a.bmask = 2047u;
     a.row_lanes = 1;  // one row per wave: measured fastest
-    if (const char* e = getenv("TMPT_ROW_LANES")) a.row_lanes = std::max(1, std::min(64, atoi(e)));
     return a;
 }
 
-template <bool WIDE, bool ROW, bool COUNT>
+
+template <bool ROW, bool COUNT>
 int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long* counters)
 {
-    auto fn = k_mega<WIDE, ROW, COUNT, kBlk, kSL>;
+    auto fn = k_mega<ROW, COUNT, kBlk, kSL>;
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // ROW: one wave per row_lanes rows (up to the resident grid)
     int64_t items = ROW ? ((int64_t)a.tile_rows + a.row_lanes - 1) / a.row_lanes * 64 : a.slots;
@@ -1689,30 +1546,15 @@ int launch_mega(Scene& s, const RenderArgs& a, uint32_t* out, unsigned long long
     return 0;
 }
 
-// BVH layout used by the traversal kernels: the 4-wide quantised BVH unless
-// TMPT_BVH=2 selects the plain LBVH2 (kept for A/B measurements).
-bool use_wide()
-{
-    const char* e = getenv("TMPT_BVH");
-    return !(e && atoi(e) == 2);
-}
-
 }  // namespace
 
 int render_megakernel(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
 {
     const bool row = a.seed_mode == TMPT_SEED_ROW;
-    const bool wide = use_wide();
-#define TMPT_MEGA(W_, R_, C_) \
-    if (wide == W_ && row == R_ && count == C_) return launch_mega<W_, R_, C_>(s, a, d_out, d_counters);
-    TMPT_MEGA(true, true, true) TMPT_MEGA(true, true, false) TMPT_MEGA(true, false, true)
-    TMPT_MEGA(true, false, false) TMPT_MEGA(false, true, true) TMPT_MEGA(false, true, false)
-    TMPT_MEGA(false, false, true) TMPT_MEGA(false, false, false)
-#undef TMPT_MEGA
-    return -1;
+    if (row) return count ? launch_mega<true, true>(s, a, d_out, d_counters) : launch_mega<true, false>(s, a, d_out, d_counters);
+    return count ? launch_mega<false, true>(s, a, d_out, d_counters) : launch_mega<false, false>(s, a, d_out, d_counters);
 }
-
 // Wavefront driver.  The host enqueues iterations without reading the queue
 // sizes (the kernels read them from device memory) and checks for completion
 // every kCheck iterations.
@@ -1723,41 +1565,9 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
         set_error("wavefront: tile too large");
         return -22;
     }
-    const bool wide = use_wide();
-    auto trace_e = wide ? (count ? k_wf_trace<true, false, true, kBlk, kSL> : k_wf_trace<true, false, false, kBlk, kSL>)
-                        : (count ? k_wf_trace<false, false, true, kBlk, kSL> : k_wf_trace<false, false, false, kBlk, kSL>);
-    auto trace_s = wide ? (count ? k_wf_trace<true, true, true, kBlk, kSL> : k_wf_trace<true, true, false, kBlk, kSL>)
-                        : (count ? k_wf_trace<false, true, true, kBlk, kSL> : k_wf_trace<false, true, false, kBlk, kSL>);
-    int sl = kSL;
-    // TMPT_TUNE=<sl>,<steps>,<refill>: tuning variants of the traversal kernels
-    if (const char* tune = getenv("TMPT_TUNE")) {
-        int a0 = 0, a1 = 0, a2 = 0, a3 = 1;
-        if (sscanf(tune, "%d,%d,%d,%d", &a0, &a1, &a2, &a3) >= 3 && !count) {
-#define TMPT_VARIANT(SL_, ST_, RF_, MW_)                                   \
-    if (wide && a0 == SL_ && a1 == ST_ && a2 == RF_ && a3 == MW_) {         \
-        trace_e = k_wf_trace<true, false, false, kBlk, SL_, ST_, RF_, MW_>; \
-        trace_s = k_wf_trace<true, true, false, kBlk, SL_, ST_, RF_, MW_>;  \
-        sl = SL_;                                                          \
-    }
-            TMPT_VARIANT(16, 4, 8, 6)
-            TMPT_VARIANT(16, 4, 8, 8)
-            TMPT_VARIANT(8, 4, 8, 6)
-            TMPT_VARIANT(8, 4, 8, 8)
-            TMPT_VARIANT(24, 4, 8, 1)
-            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 0) {  // no vote (both step kinds per round)
-                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 8, 1, 0, 1, 0>;
-                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 0, 0, 0>;
-            }
-            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 200) {  // nearest-first any-hit
-                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 0, 1>;
-            }
-            if (wide && a0 == 16 && a1 == 4 && a2 == 8 && a3 == 100) {  // probing segment fetch
-                trace_e = k_wf_trace<true, false, false, kBlk, 16, 4, 8, 1, 1>;
-                trace_s = k_wf_trace<true, true, false, kBlk, 16, 4, 8, 1, 1>;
-            }
-#undef TMPT_VARIANT
-        }
-    }
+    auto trace_e = count ? k_wf_trace<false, true, kBlk, kSL> : k_wf_trace<false, false, kBlk, kSL>;
+    auto trace_s = count ? k_wf_trace<true, true, kBlk, kSL> : k_wf_trace<true, false, kBlk, kSL>;
+    const int sl = kSL;
     int grid_t = occupancy_grid((const void*)trace_e, kBlk, 0, s.device);
     const int grid_sh = (int)((P + kBlk - 1) / kBlk);
     const size_t seg_cap = (size_t)(((P + kSeg - 1) / kSeg + kBlk - 1) / kBlk) * kBlk;
@@ -1773,7 +1583,11 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
            o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(qcap), o_q1 = take(qcap),
            o_qs = take(qcap), o_ctl = take(5 * ctr_words + 64), o_tot = take(16),
            o_ovf = take(ovf_words);
-    const bool log_iters = getenv("TMPT_ITER_LOG") != nullptr;
+#ifdef TMPT_DIAG
+    const bool log_iters = getenv("TMPT_ITER_LOG") != nullptr;  // diagnostic build: queue sizes per iteration
+#else
+    const bool log_iters = false;
+#endif
     const int64_t max_log = (int64_t)a.spp * (kMaxDepth + 2) + 64 + 16;
     size_t o_log = log_iters ? take(2 * (size_t)max_log) : 0;
     if (ensure_ws(s, words * 4)) return -1;
@@ -1888,103 +1702,48 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
 int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
 {
+    const Options& o = s.opt;
     // HIP events around each k_path launch (pilot: 0-1, final: 2-3) on the
     // stream it runs on: the dominant kernel's own time for the roofline
     if (!s.path_ev[0])
         for (auto& e : s.path_ev) TMPT_HIP(hipEventCreate(&e));
     // traversal rounds between shading checks / lanes waiting that trigger a
-    // shading round (A/B on the bench frame at 1 and 8 shards, tools/tune.py)
-    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16;
-    // node step (TMPT_NODE, A/B): q = BVH4Q min/max decode, f = BVH4F f32 boxes,
-    // s = BVH4Q octant decode + full near-to-far sort, n = octant decode,
-    // nearest child first (others pairwise ordered), default = n with the top
-    // kTopNodes nodes read from a per-block LDS copy
-    const char* nf = getenv("TMPT_NODE");
-    const char nc = nf ? nf[0] : 't';
-    const int fmt = nc == 'q' ? 0 : (nc == 'f' ? 1 : (nc == 's' ? 2 : (nc == 'n' ? 3 : 4)));
+    // shading round (A/B on the bench frame at 1 and 8 shards);
     // sparse-wave shading threshold divisor (k_path TAIL): 2 -- bench frame,
-    // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms)
-    constexpr int kSparse = 2;
-    using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 2>);
-    PathFn fn = nullptr;
-#define TMPT_PF(C_, F_) \
-    if (count == C_ && fmt == F_) fn = k_path<C_, kBlk, kPathSL, kPathSteps, kShadeMin, 1, F_, 4, kSparse>;
-    TMPT_PF(true, 0) TMPT_PF(true, 1) TMPT_PF(true, 2) TMPT_PF(true, 3) TMPT_PF(true, 4)
-    TMPT_PF(false, 0) TMPT_PF(false, 1) TMPT_PF(false, 2) TMPT_PF(false, 3) TMPT_PF(false, 4)
-#undef TMPT_PF
-    // TMPT_TUNE=903,<sparse>: the pixel-mode kernel with another sparse-wave divisor (A/B)
-    if (const char* tune = getenv("TMPT_TUNE")) {
-        int t0 = 0, t1 = 0;
-        if (sscanf(tune, "%d,%d", &t0, &t1) == 2 && t0 == 903 && !count && fmt == 4) {
-            if (t1 == 4) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, 4>;
-            if (t1 == 1) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, 1>;
-        }
-    }
+    // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms);
+    // sample seeding 220.4 -> 218.2 ms at N=1, 29.4 -> 29.0 ms at 1/8
+    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
+    using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
+    // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
+    // kernel keeps its register allocation)
+    PathFn fn = a.jt ? (count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>
+                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>)
+                     : (count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>
+                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     const PathFn fn_default = fn;
-    // TMPT_PROF=1 (diagnostic): s_memtime split of wave time (shading / node / leaf rounds)
-    const char* pe = getenv("TMPT_PROF");
-    const bool prof = pe && atoi(pe) != 0 && !count && fmt == 4;
-    // TMPT_PROF=2: + shading-round split; 3: + per-round cycle counts (more registers:
-    // the kernel may drop to 3 waves/SIMD, so compare its times only among PROF=3 runs)
-    if (prof) fn = atoi(pe) >= 3 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 3>
-                   : atoi(pe) == 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 2>
-                                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparse, 1>;
-    // TMPT_TUNE=900,<steps>,<shade_min>,<vote>,<tail steps>: tuning variants of the path kernel
-    if (const char* tune = getenv("TMPT_TUNE")) {
-        int a0 = 0, a1 = 0, a2 = 0, a3 = 1, a4 = 0;
-        if (sscanf(tune, "%d,%d,%d,%d,%d", &a0, &a1, &a2, &a3, &a4) >= 4 && a0 == 900 && !count) {
-#define TMPT_PV(ST_, SM_, V_, T_)                                                  \
-    if (a1 == ST_ && a2 == SM_ && a3 == V_ && a4 == T_)                           \
-        fn = fmt == 4 ? k_path<false, kBlk, kPathSL, ST_, SM_, V_, 4, 1, T_>           \
-                      : k_path<false, kBlk, kPathSL, ST_, SM_, V_, 3, 1, T_>;
-            TMPT_PV(8, 8, 1, 2) TMPT_PV(8, 8, 2, 2) TMPT_PV(16, 16, 1, 2) TMPT_PV(16, 16, 2, 4)
-            TMPT_PV(32, 32, 1, 4) TMPT_PV(16, 8, 1, 2) TMPT_PV(16, 8, 1, 4) TMPT_PV(12, 12, 1, 4)
-            TMPT_PV(20, 16, 1, 4)
-#undef TMPT_PV
-        }
-    }
-    if (a.jt) {  // sample seeding: its own instantiation (the pixel-mode kernel keeps its registers)
-        // sparse-wave divisor 2 (shade once half of the lanes still holding work
-        // wait, when fewer than 32 hold any): bench frame 220.4 -> 218.2 ms at N=1,
-        // 29.4 -> 29.0 ms at the 1/8 shard (TMPT_TUNE=902 sweep)
-        constexpr int kSparseS = kSparse;
-        fn = count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>
-                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparseS, 0, 0, 1>;
-        // TMPT_SAMPLE_OCC=5 (A/B): 5 waves per SIMD, light terms and the pending
-        // ray in global memory (k_path kGL)
-        if (const char* e = getenv("TMPT_SAMPLE_OCC"))
-            if (atoi(e) == 5 && !count) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 5, kSparseS, 0, 0, 1>;
-        if (prof)  // TMPT_PROF=1|2 (diagnostic): wave-time split of the sample kernel
-            fn = atoi(pe) >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 2, 0, 1>
-                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 1, kSparseS, 1, 0, 1>;
-        // TMPT_TUNE=902,<steps>,<shade_min>,<sparse>: round-cadence variants of the sample kernel (A/B)
-        if (const char* tune = getenv("TMPT_TUNE")) {
-            int t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-            if (sscanf(tune, "%d,%d,%d,%d", &t0, &t1, &t2, &t3) == 4 && t0 == 902 && !count) {
-#define TMPT_SV(ST_, SM_, SP_) \
-    if (t1 == ST_ && t2 == SM_ && t3 == SP_) fn = k_path<false, kBlk, kPathSL, ST_, SM_, 1, 4, 4, SP_, 0, 0, 1>;
-                TMPT_SV(16, 16, 4) TMPT_SV(16, 16, 2) TMPT_SV(16, 16, 1) TMPT_SV(16, 16, 3) TMPT_SV(16, 20, 2)
-                TMPT_SV(20, 20, 2) TMPT_SV(20, 16, 2) TMPT_SV(16, 24, 2) TMPT_SV(16, 24, 1) TMPT_SV(16, 32, 1)
-#undef TMPT_SV
-            }
-        }
-    }
-    int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
-    // TMPT_BLOCKS_PER_CU=<b> (A/B): fewer resident blocks than the occupancy allows
-    if (const char* e = getenv("TMPT_BLOCKS_PER_CU")) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) == hipSuccess && cus > 0 &&
-            atoi(e) > 0)
-            grid = std::min(grid, atoi(e) * cus);
-    }
+    int prof = 0;
+#ifdef TMPT_DIAG
+    // diagnostic build only: TMPT_PROF=1 s_memtime split of wave time (shading /
+    // node / leaf rounds); 2: + shading-round split; 3: + per-round cycle counts
+    // (more registers: compare its times only among PROF=3 runs)
+    if (const char* pe = getenv("TMPT_PROF")) prof = count ? 0 : atoi(pe);
+    if (prof && !a.jt)
+        fn = prof >= 3 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 3>
+           : prof == 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 2>
+                       : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 1>;
+    if (prof && a.jt)
+        fn = prof >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 2, 0, 1>
+                       : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 1, 0, 1>;
+#endif
+    const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // Sample seeding: the work units are (pixel, block of blk samples).  The
     // block is the largest power of two that still leaves >= kUnitsPerLane
     // units per resident lane (the frame's tail is then one block of the
-    // heaviest pixel, not its whole sample chain).  Bench frame (tools/tune.py,
-    // 1-row bands, k_path ms): N=1 blk 2/4/8 = 220.7/217.8/217.3; 1/2 shard
-    // blk 1/2/4/8 = 113.3/110.9/110.2/111.7; 1/4 blk 1/2/4 = 57.1/56.2/56.6;
-    // 1/8 blk 1/2/4/8 = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane, so
-    // 60 picks 8, 4, 2, 1 at N = 1, 2, 4, 8.  TMPT_SAMPLE_BLOCK=<b>.
+    // heaviest pixel, not its whole sample chain).  Bench frame (1-row bands,
+    // k_path ms): N=1 blk 2/4/8 = 220.7/217.8/217.3; 1/2 shard blk 1/2/4/8 =
+    // 113.3/110.9/110.2/111.7; 1/4 blk 1/2/4 = 57.1/56.2/56.6; 1/8 blk 1/2/4/8
+    // = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane, so 60 picks 8, 4,
+    // 2, 1 at N = 1, 2, 4, 8.  Option sample_block fixes it.
     uint32_t blk = 1u, nblk = 1u;
     if (a.jt) {
         constexpr int64_t kUnitsPerLane = 60;
@@ -1993,22 +1752,19 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)a.spp &&
                a.slots * (((int64_t)a.spp + blk * 2 - 1) / (blk * 2)) >= kUnitsPerLane * lanes0)
             blk *= 2u;
-        if (const char* e = getenv("TMPT_SAMPLE_BLOCK")) {
-            const int b = atoi(e);
-            if (b >= 1 && b <= 1024 && (b & (b - 1)) == 0) blk = (uint32_t)b;
-        }
+        if (o.sample_block > 0) blk = (uint32_t)o.sample_block;
         while (a.slots * (((int64_t)a.spp + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
         nblk = (uint32_t)(((int64_t)a.spp + blk - 1) / blk);
         // Several blocks per pixel need the per-sample colour buffer (16 B per
         // sample of the tile: 2.1 GB at 1080p x 64).  If it does not fit in 3/4
-        // of the free device memory (or TMPT_SBUF_MAX bytes), the pixel is one
+        // of the free device memory (or the sbuf_max option), the pixel is one
         // unit: same image, only the tail of a small shard is longer.
         if (nblk > 1) {
             const size_t need = sizeof(float4) * (size_t)a.spp * (size_t)a.slots;
             size_t fr = 0, tot = 0;
             size_t budget = hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0;
             budget += s.sbuf_bytes;  // the buffer already held is free for this call
-            if (const char* e = getenv("TMPT_SBUF_MAX")) budget = std::min(budget, (size_t)strtoull(e, nullptr, 10));
+            if (o.sbuf_max > 0.0) budget = std::min(budget, (size_t)o.sbuf_max);
             if (need > budget) {
                 while (blk < (uint32_t)a.spp) blk *= 2u;
                 nblk = 1u;
@@ -2018,74 +1774,47 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const int64_t P = a.slots * (int64_t)nblk;  // units the supply hands out
     // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
     // a shard has several pixels per resident lane, the frame ends with the
-    // chains of the pixels started last.  A first pass runs kPilot samples of
+    // chains of the pixels started last.  A first pass runs `pilot` samples of
     // every pixel and records its traversal steps; the remaining samples run
     // with pixels handed out most expensive first (3x3-smoothed pilot cost).
     // The passes continue each pixel's RNG stream and colour sum exactly as
     // progressive spp does, so the image is the single-pass image bit for bit.
-    // TMPT_PILOT=<samples> (0 = off).
-    // TMPT_PILOT_RATIO: minimum pixels per resident lane for the ordering (x10).
     // 4 pilot samples; 2 at low load (at most ~2.5 pixels per resident lane,
     // where the pilot pass is a tail of its own: 1/8 shard 42.2 -> 41.3 ms,
-    // 1/4 74.6 -> 73.5 ms)
-    int pilot = 2 * P <= 5 * (int64_t)grid * kBlk ? 2 : 4, ratio10 = 0;
-    if (const char* e = getenv("TMPT_PILOT")) pilot = std::max(0, atoi(e));
-    if (const char* e = getenv("TMPT_PILOT_RATIO")) ratio10 = std::max(0, atoi(e));
+    // 1/4 74.6 -> 73.5 ms).  Option pilot (0 = off).
+    int pilot = 2 * P <= 5 * (int64_t)grid * kBlk ? 2 : 4;
+    if (o.pilot >= 0) pilot = o.pilot;
     const bool ordered = pilot > 0 && !count && !a.jt && a.smp_begin == 0 && a.smp_end == a.spp &&
-                         a.spp >= 2 * pilot && 10 * P >= (int64_t)ratio10 * grid * kBlk && P < (1ll << 31);
+                         a.spp >= 2 * pilot && P < (1ll << 31);
     // Shadow offload at low load (k_path HELP): with at most ~2.5 pixels per
     // resident lane the frame is bound by the most expensive pixels' chains, and
     // 27-28 % of their traversal work is shadow queries, which feed neither the
     // RNG stream nor the path (main.cpp:57-67).  Lanes without a pixel then trace
     // other lanes' shadow queries, and (ordered passes) each 64-rank chunk pairs
     // `pair` expensive ranks with 64-pair cheap ones, whose lanes free up early.
-    // Bench frame (tools/tune.py, TUNE_SHARDS): 1/4 shard 86.4 -> 77.2 ms (pair
-    // 56), 1/8 shard 45.7 -> 43.9 ms (pair 52); at 1/2 and 1/1 it loses (the
-    // extra shading code), so it is off there.  TMPT_HELP=0|1 and TMPT_PAIR=<h>
-    // override the choice.
+    // Bench frame: 1/4 shard 86.4 -> 77.2 ms (pair 56), 1/8 shard 45.7 -> 43.9 ms
+    // (pair 52); at 1/2 and 1/1 it loses (the extra shading code), so it is off
+    // there.  Options help and pair override the choice.
     const int64_t lanes = (int64_t)grid * kBlk;
-    int help = ordered && fn == fn_default && fmt == 4 && 2 * P <= 5 * lanes ? 1 : 0;
-    if (const char* e = getenv("TMPT_HELP")) help = atoi(e) != 0 && !count && fmt == 4 && !prof && !a.jt;
+    int help = ordered && fn == fn_default && 2 * P <= 5 * lanes ? 1 : 0;
+    if (o.help >= 0) help = o.help != 0 && !count && !prof && !a.jt;
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
-    if (const char* e = getenv("TMPT_PAIR")) pair = atoi(e);
-    if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 1>;
+    if (o.pair >= 0) pair = o.pair;
+    if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
     const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
     const size_t reg_words = ordered ? 2 * (size_t)kSimdKeys + 64 + (size_t)P : 0;  // + claim words
     const size_t extra_words = ordered ? (size_t)P * (4 + 5) + hist_words + reg_words : 0;
-    const bool gl = fn == (PathFn)k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 5, kSparse, 0, 0, 1>;
-    const size_t gl_words = gl ? (size_t)grid * kBlk * (kMaxDepth + 6) : 0;
-    if (ensure_ws(s, (ovf_words + head_words + extra_words + gl_words) * 4)) return -1;
+    if (ensure_ws(s, (ovf_words + head_words + extra_words) * 4)) return -1;
     uint32_t* heads = (uint32_t*)s.ws + ovf_words;
     TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
     PathCtl pc;
-    // TMPT_COST_MAP=1 (diagnostic, instrumented renders only): the output
-    // receives each pixel's traversal work (node visits + triangle tests)
-    const char* cm = getenv("TMPT_COST_MAP");
-    pc.cost_map = count && cm ? atoi(cm) : 0;  // 2: shadow-query work only
+    memset(&pc, 0, sizeof(pc));
     pc.heads = heads;
     pc.P = P;
-    pc.simd_reg = nullptr;
-    pc.claim = nullptr;
-    pc.nsimd = pc.wps = 0;
-
-    pc.order = nullptr;
-    pc.cost_out = nullptr;
-    pc.tlog = nullptr;
-    pc.prio_q = 0;
-    pc.dprio[0] = pc.dprio[1] = pc.dprio[2] = 0.0f;
-    pc.dprio_cost = nullptr;
-    pc.diag_noshadow = getenv("TMPT_DIAG_NOSHADOW") ? atoi(getenv("TMPT_DIAG_NOSHADOW")) : 0;
     pc.nblk = nblk;
     pc.blk = blk;
-    pc.sbuf = nullptr;
-    pc.upix = pc.ustate = pc.uslot = nullptr;
-    pc.rs_out = nullptr;
-    pc.rs_end = nullptr;
-    pc.p_dev = nullptr;
-    pc.rs_noshadow = 0;
-    pc.gl_store = gl ? reinterpret_cast<float*>((uint32_t*)s.ws + ovf_words + head_words + extra_words) : nullptr;
     RenderArgs as = a;  // sample seeding: a lane's run of samples is its block
     if (a.jt) {
         as.bmask = nblk > 1 ? blk - 1u : 2047u;
@@ -2101,71 +1830,37 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             pc.sbuf = s.sbuf;
         }
     }
-    // sbuf layout (TMPT_SBUF, A/B): 0 = [sample][pixel], 1 = [pixel][sample],
-    // 2 = [pixel][sample] with nontemporal stores (default: a 16-B store into
-    // [sample][pixel] pulls its whole line into L2 -- 27 GB of extra fetches
-    // per 1080p frame -- while nontemporal stores of a pixel's runs do not;
-    // k_resolve_px reads the pixel-major buffer through LDS)
-    int sbl = 2;
-    if (const char* e = getenv("TMPT_SBUF")) sbl = atoi(e);
-    pc.sb_nt = sbl == 2;
-    if (sbl >= 1) {
-        pc.sb_ss = 1u;
-        pc.sb_sp = (uint32_t)a.spp;
-    } else {
-        pc.sb_ss = (uint32_t)a.slots;
-        pc.sb_sp = 1u;
-    }
+    // sbuf is [pixel][sample] with nontemporal stores (a 16-B store into a
+    // [sample][pixel] line pulled the whole line into L2 -- 27 GB of extra
+    // fetches per 1080p frame); k_resolve_px reads it through LDS
+    pc.sb_ss = 1u;
+    pc.sb_sp = (uint32_t)a.spp;
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
     // slots and each wave's chain -- the frame's critical path at that load --
     // has fewer lanes to interleave (bench frame, 1/32 shard: 44.1 -> 40.9 ms;
     // at 1/16 (half the lanes) it measured 44.4 -> 45.5 ms, so not there; 16
-    // lanes per wave was slower still).  TMPT_WAVE_CAP=<c> fixes the cap (64 = off).
+    // lanes per wave was slower still).  Option wave_cap fixes the cap.
     {
         const int64_t waves = std::max<int64_t>(1, (int64_t)grid * (kBlk / 64));
         int64_t c = P <= waves * 16 ? 32 : 64;
-        if (const char* e = getenv("TMPT_WAVE_CAP")) c = atoi(e);
+        if (o.wave_cap > 0) c = o.wave_cap;
         pc.lane_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(64, c));
     }
     pc.chunk = std::min<uint32_t>(kChunk, pc.lane_cap);
     pc.nchunks = (uint32_t)((P + pc.chunk - 1) / pc.chunk);
-    // TMPT_TLOG=<file>: per-pixel {start, end, steps, shading rounds} (the
-    // shading-round count in PROF builds only)
-    // of the final launch, s_memrealtime ticks (100 MHz), written as raw u32
-    const char* tl = getenv("TMPT_TLOG");
     auto final_launch = [&](const RenderArgs& af) -> int {
-        uint32_t* d_tlog = nullptr;
-        if (tl) {
-            TMPT_HIP(hipMalloc(&d_tlog, (size_t)P * 16));
-            TMPT_HIP(hipMemsetAsync(d_tlog, 0, (size_t)P * 16, s.stream));
-        }
-        pc.tlog = d_tlog;
         TMPT_HIP(hipEventRecord(s.path_ev[2], s.stream));
         fn<<<grid, kBlk, 0, s.stream>>>(view(s), af, pc, d_out, (uint32_t*)s.ws, d_counters);
         TMPT_HIP(hipGetLastError());
         TMPT_HIP(hipEventRecord(s.path_ev[3], s.stream));
-        if (tl) {
-            std::vector<uint32_t> h((size_t)P * 4);
-            TMPT_HIP(hipStreamSynchronize(s.stream));
-            TMPT_HIP(hipMemcpy(h.data(), d_tlog, (size_t)P * 16, hipMemcpyDeviceToHost));
-            (void)hipFree(d_tlog);
-            if (FILE* f = fopen(tl, "wb")) {
-                fwrite(h.data(), 4, h.size(), f);
-                fclose(f);
-            }
-        }
         return 0;
     };
     if (!ordered) {
         if (final_launch(as)) return -1;
         if (pc.sbuf) {
-            if (pc.sb_ss == 1u)
-                k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(pc.sbuf, a.slots, a.spp,
-                                                                                 a.spp_recip, d_out);
-            else
-                k_resolve<<<(unsigned)((a.slots + 255) / 256), 256, 0, s.stream>>>(pc.sbuf, a.slots, a.spp, pc.sb_ss,
-                                                                                 pc.sb_sp, a.spp_recip, d_out);
+            k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(pc.sbuf, a.slots, a.spp,
+                                                                             a.spp_recip, d_out);
             TMPT_HIP(hipGetLastError());
         }
         s.path_launches = 1;
@@ -2205,10 +1900,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // SIMD-balanced first chunks (PathCtl::simd_reg): with the chunks in
     // descending cost, the resident waves of every SIMD take one chunk from
     // each quarter, alternating ends, instead of the launch order's heaviest or
-    // lightest of every quarter.  TMPT_BALANCE=0|1.
-    int balance = 1;
-    if (const char* e = getenv("TMPT_BALANCE")) balance = atoi(e) != 0;
-    if (balance) {
+    // lightest of every quarter.  Option balance.
+    if (o.balance) {
         int dev_cus = 0;
         if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
             dev_cus < 1)
@@ -2220,34 +1913,18 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         pc.claim = simd_reg + 2 * (size_t)kSimdKeys + 64;
         TMPT_HIP(hipMemsetAsync(simd_reg, 0, reg_words * 4, s.stream));
     }
-    // TMPT_PRIO=<d>: waves holding ranks of the first d-th of the order issue at
-    // priority 3, the next d-th at 2, the next at 1 (0 = off)
-    if (const char* e = getenv("TMPT_PRIO")) {
-        const int d = atoi(e);
-        if (d > 0) pc.prio_q = (uint32_t)std::max<int64_t>(1, (P + d - 1) / d);
-    }
     // Dynamic priority (PathCtl::dprio) at low load (with the helpers): the
     // heaviest waves start at the top level and step down as their projected
     // remaining work falls below 32 / 21 / 10.5 % of the heaviest pixel's, so
     // the issue slots go to the waves with the most work left instead of to
     // the oldest.  Bench frame, 1/8 shard 44.9 -> 42.4 ms, 1/4 78.9 -> 75.3 ms
     // (with the balanced first chunks); at one pixel pass per lane or more it
-    // costs ~0.4 %, so it is off there.  TMPT_DPRIO=<t3>,<t2>,<t1>: absolute
-    // thresholds in steps (0,0,0 = off).
-    if (help) {
+    // costs ~0.4 %, so it is off there.  Option dprio.
+    if (help && o.dprio) {
         pc.dprio[0] = 0.32f;
         pc.dprio[1] = 0.21f;
         pc.dprio[2] = 0.105f;
         pc.dprio_cost = cost;
-    }
-    if (const char* e = getenv("TMPT_DPRIO")) {
-        float t3 = 0, t2 = 0, t1 = 0;
-        if (sscanf(e, "%f,%f,%f", &t3, &t2, &t1) == 3) {
-            pc.dprio[0] = t3;
-            pc.dprio[1] = t2;
-            pc.dprio[2] = t1;
-            pc.dprio_cost = nullptr;
-        }
     }
     if (final_launch(a2)) return -1;
     s.path_launches = 2;
@@ -2262,13 +1939,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 // the host only checks for completion every kCheck iterations.
 int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
 {
+    const Options& o = s.opt;
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2, kCheck = 64;
-    auto fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 4, kSparse, 0, 0, 2>;
+    auto fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
     // the shadow-free pass: its own instantiation (no shadow, light or colour
-    // code, no light / next-ray LDS)
-    auto fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, kRsOcc3, kSparse, 0, 0, 3>;
-    if (const char* e = getenv("TMPT_ROWSPEC_OCC"))  // A/B: 6 waves per SIMD (80 VGPRs, 21 spilled dwords)
-        if (atoi(e) == 6) fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, 4, 6, kSparse, 0, 0, 3>;
+    // code, no light / next-ray LDS): 96 VGPRs, 5 waves per SIMD (6 waves: 80
+    // VGPRs and 21 spilled dwords, neutral)
+    auto fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 3>;
     const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     const int grid3 = occupancy_grid((const void*)fn3, kBlk, 0, s.device);
     const int rows = a.tile_rows;
@@ -2277,24 +1954,15 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // ~25; a cap of 24 draws left those rows one short window per pixel, and
     // the slowest row sets the iteration count)
     uint32_t wmax = (uint32_t)std::min<int64_t>(8192, std::max<int64_t>(64, (int64_t)a.spp * 24));
-    if (const char* e = getenv("TMPT_ROWSPEC_WMAX")) wmax = (uint32_t)std::max(8, std::min(16384, atoi(e)));
-    float margin = 1.1f;  // window = expected draws x margin (1.05 / 1.1 / 1.15: 3.17 / 3.11 / 3.21 s)
-    if (const char* e = getenv("TMPT_ROWSPEC_MARGIN")) margin = std::max(0.1f, (float)atof(e));
-    int G = 2;  // row groups (streams)
-    if (const char* e = getenv("TMPT_ROWSPEC_GROUPS")) G = atoi(e);
-    G = std::max(1, std::min(std::min(G, kRowSpecMaxGroups), rows));
-    // each group's k_path gets grid / gdiv blocks: with gdiv = G the groups'
-    // kernels share the GPU at once instead of queueing behind each other
-    int gdiv = 1;
-    if (const char* e = getenv("TMPT_ROWSPEC_GDIV")) gdiv = std::max(1, std::min(16, atoi(e)));
-    const int pgrid = std::max(1, grid / gdiv);
-    const int pgrid3 = std::max(1, grid3 / gdiv);
-    // units a wave reserves at once (a launch holds ~1.5 units per lane, so
-    // smaller reservations balance the waves' loads)
-    uint32_t chunk = kChunk;
-    if (const char* e = getenv("TMPT_ROWSPEC_CHUNK")) chunk = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    // lookahead windows (pixels x+1, x+2, ...; each from look_lo of its
-    // expected start): one iteration covers up to nwin pixels of a row.  The
+    if (o.rowspec_wmax > 0) wmax = (uint32_t)o.rowspec_wmax;
+    // row groups, each on its own stream (one group: 3 % slower)
+    const int G = std::max(1, std::min(std::min(o.rowspec_groups, kRowSpecMaxGroups), rows));
+    // every group's k_path gets the whole resident grid (splitting the GPU
+    // between the groups, or reserving fewer than 64 units per wave, did not help)
+    const int pgrid = grid, pgrid3 = grid3;
+    const uint32_t chunk = kChunk;
+    // lookahead windows (pixels x+1, x+2, ...; each around its expected
+    // start and end): one iteration covers up to nwin pixels of a row.  The
     // extra speculation is cheap while the GPU has room: nwin ~ 5 units per
     // resident lane over the rows' expected pixel windows (~17 draws per
     // sample), 2..kRsMaxWin -- 2 on the whole bench frame, 8 from 1/4 of it.
@@ -2307,16 +1975,13 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     const double E_est = (double)a.spp * 8.5;
     int nwin = (int)std::lround(std::min((double)lanes * 5.0 / ((double)rows * E_est), 4400.0 / E_est));
     nwin = std::max(2, std::min(kRsMaxWin, nwin));
-    if (const char* e = getenv("TMPT_ROWSPEC_LOOK")) nwin = std::max(1, std::min(kRsMaxWin, atoi(e) + 1));
-    float look_lo = 0.9f;  // 0.75 / 0.85 / 0.9 / 0.95 at margin 1.15: 3.24 / 3.18 / 3.18 / 3.22 s
-    if (const char* e = getenv("TMPT_ROWSPEC_LO")) look_lo = std::max(0.0f, std::min(1.0f, (float)atof(e)));
+    if (o.rowspec_windows > 0) nwin = std::min(kRsMaxWin, o.rowspec_windows);
     const uint32_t jmax = (uint32_t)nwin * wmax;  // window i ends by (i + 1) * wmax
     // Speculate without shadow traversals and re-trace the chain in full at the
     // end (the frame's chain list and colour buffer must fit; else the colours
     // come from the speculative pass).  Bench frame 3.03 -> 2.49 s, 1/8 shard
-    // 0.71 -> 0.61 s (profiles/r02_rowspec/rs19).  TMPT_ROWSPEC_NOSHADOW=0: off
-    bool noshadow = true;
-    if (const char* e = getenv("TMPT_ROWSPEC_NOSHADOW")) noshadow = atoi(e) != 0;
+    // 0.71 -> 0.61 s (profiles/r02_rowspec/rs19).  Option rowspec_noshadow.
+    bool noshadow = o.rowspec_noshadow != 0;
     const size_t lcap = (size_t)a.slots * (size_t)a.spp;  // chain samples of the tile
     const uint32_t scap = (uint32_t)nwin * (uint32_t)a.spp;  // a row's chain samples per iteration
     if (noshadow) {
@@ -2423,18 +2088,14 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.rs.row0 = row0;
         q.rs.nrows = (int)R;
         q.rs.wmax = wmax;
-        q.rs.margin = margin;
         q.rs.nwin = nwin;
         // window placement: expected positions +- spread * sqrt(i) pixels;
         // bench frame, 64 spp (profiles/r02_rowspec/rs15): spread 0.08 / 0.1 /
         // 0.12 / 0.15 = 3.06 / 3.03 / 3.04 / 3.10 s whole, 0.85 / 0.74 / 0.69 /
-        // 0.67 s at 1/8 -- wider at low load, where speculation is cheap.
-        // TMPT_ROWSPEC_SPREAD=0: the linear placement (look_lo, margin)
+        // 0.67 s at 1/8 -- wider at low load, where speculation is cheap
         // (with shadow-free speculation: 1/8 shard spread 0.154 / 0.2 = 640 / 576 ms,
         // whole frame 0.106 / 0.14 / 0.2 = 2.51 / 2.52 / 2.62 s, rs20)
-        q.rs.spread = 0.07f + 0.016f * (float)nwin;
-        if (const char* e = getenv("TMPT_ROWSPEC_SPREAD")) q.rs.spread = std::max(0.0f, (float)atof(e));
-        q.rs.look_lo = look_lo;
+        q.rs.spread = o.rowspec_spread >= 0.0f ? o.rowspec_spread : 0.07f + 0.016f * (float)nwin;
         row0 += (int)R;
         q.rs_out = reinterpret_cast<float4*>(gp);
         gp += q.U * sizeof(float4);
@@ -2536,13 +2197,13 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         pc2.sbuf = s.sbuf;
         pc2.sb_ss = 1u;
         pc2.sb_sp = (uint32_t)a.spp;
-        pc2.sb_nt = 1;
         TMPT_HIP(hipMemsetAsync(gs[0].heads, 0, head_words * 4, s.stream));
         fn<<<pgrid, kBlk, 0, s.stream>>>(view(s), as, pc2, d_out, gs[0].ovf, spec_ctr + 16);
         k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(s.sbuf, a.slots, a.spp, a.spp_recip, d_out);
         TMPT_HIP(hipGetLastError());
     }
     s.path_launches = it;
+#ifdef TMPT_DIAG
     if (getenv("TMPT_ROWSPEC_LOG")) {
         unsigned long long c[2] = {0, 0};
         TMPT_HIP(hipMemcpyAsync(c, d_counters, sizeof(c), hipMemcpyDeviceToHost, s.stream));
@@ -2571,24 +2232,21 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
             swmax = std::max(swmax, v);
         }
         fprintf(stderr,
-                "rowspec: %d iterations enqueued, %d groups of %d blocks, window cap %u, margin %.2f, traced rays "
+                "rowspec: %d iterations enqueued, %d groups of %d blocks, window cap %u, %d windows, traced rays "
                 "%llu for %llu chain rays (x%.2f); short windows per row: mean %.1f max %u\n",
-                it, G, pgrid, wmax, margin, t, c[0], c[0] ? (double)t / (double)c[0] : 0.0,
+                it, G, pgrid, wmax, nwin, t, c[0], c[0] ? (double)t / (double)c[0] : 0.0,
                 rows ? (double)swsum / rows : 0.0, swmax);
     }
+#endif
     return 0;
 }
 
-int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any,
+// rays: n x 6 floats (one [tmin, tmax] for all) or, ranged, n x 8 (per ray)
+int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any, bool ranged,
                     float* d_hits, int32_t* d_ids)
 {
-    if (!use_wide() && !s.has_bvh2) {
-        set_error("TMPT_BVH=2 needs a scene built with TMPT_BUILDER=lbvh");
-        return -22;
-    }
-    const bool wide = use_wide();
-    auto fn = wide ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<true, false, kBlk, kSL>)
-                   : (any ? k_intersect<false, true, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
+    auto fn = ranged ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<false, true, kBlk, kSL>)
+                     : (any ? k_intersect<true, false, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (n + kBlk - 1) / kBlk));
     size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);
@@ -2601,10 +2259,6 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
 int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t* d_out,
            uint64_t* ray_count)
 {
-    if (!use_wide() && !s.has_bvh2) {
-        set_error("TMPT_BVH=2 needs a scene built with TMPT_BUILDER=lbvh");
-        return -22;
-    }
     RenderArgs a = make_args(cam, d);
     bool count = (d->flags & TMPT_FLAG_COUNT_VISITS) != 0;
     // progressive spp: keep per-pixel state for the shard between calls
@@ -2653,11 +2307,9 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         a.jt = s.jt;
     }
     if (d->flags & TMPT_FLAG_WAIT_STREAM) {  // order after the caller's stream (tmpt.h)
-        hipEvent_t ev;
-        TMPT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        hipError_t e = hipEventRecord(ev, reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(d->wait_stream)));
-        if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, ev, 0);
-        (void)hipEventDestroy(ev);
+        if (!s.wait_ev) TMPT_HIP(hipEventCreateWithFlags(&s.wait_ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(s.wait_ev, reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(d->wait_stream)));
+        if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, s.wait_ev, 0);
         if (e != hipSuccess) {
             set_error(std::string("tmpt_render: wait_stream: ") + hipGetErrorString(e));
             return -1;
@@ -2672,16 +2324,15 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     TMPT_HIP(hipEventCreate(&e1));
     TMPT_HIP(hipEventRecord(e0, s.stream));
     int rc = 0;
-    bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode != TMPT_SEED_ROW;
-    bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode != TMPT_SEED_ROW && use_wide();
+    const bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode != TMPT_SEED_ROW;
+    const bool persistent = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode != TMPT_SEED_ROW;
     // row seeding on the persistent engine: the speculative row chains
-    // (render_rowspec); instrumented renders and TMPT_ROWSPEC=0 run the
+    // (render_rowspec); instrumented renders and option rowspec=0 run the
     // megakernel's one lane per row
-    const char* rse = getenv("TMPT_ROWSPEC");
-    const bool rowspec = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_ROW && use_wide() &&
-                         !count && !progressive && !(rse && atoi(rse) == 0);
+    const bool rowspec = d->engine == TMPT_ENGINE_PERSISTENT && a.seed_mode == TMPT_SEED_ROW && !count &&
+                         !progressive && s.opt.rowspec != 0;
     if (progressive && !persistent) {
-        set_error("tmpt_render: progressive spp needs the persistent engine (TMPT_BVH=2 is BVH2-only)");
+        set_error("tmpt_render: progressive spp needs the persistent engine");
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         (void)hipFreeAsync(d_counters, s.stream);
@@ -2729,6 +2380,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         s.shadow_tri_tests = c[5];
         s.extend_launches = s.path_launches;  // same k_path instantiation per launch
         s.iterations = 1;
+#ifdef TMPT_DIAG
         if (c[13] + c[14] + c[15]) {
             const double tot = (double)(c[13] + c[14] + c[15]);
             fprintf(stderr, "k_path wave time: shading %.1f%%, node rounds %.1f%%, leaf rounds %.1f%% "
@@ -2744,15 +2396,13 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
                                 "query set-up %.1f%% (of all wave time)\n",
                         100.0 * c[16] / tot, 100.0 * c[17] / tot, 100.0 * c[18] / tot, 100.0 * c[19] / tot);
         }
-        if (getenv("TMPT_BALANCE_LOG"))
-            fprintf(stderr, "balance: %.2f ms, lost claims %llu, slots beyond wps %llu, no dense index %llu\n", ms,
-                    c[21], c[22], c[23]);
-        if (count && getenv("TMPT_ROUND_LOG"))  // diagnostic: wave-round efficiency
+        if (count && getenv("TMPT_ROUND_LOG"))  // wave-round efficiency
             fprintf(stderr,
                     "k_path rounds: node %llu (%.1f lanes), leaf %llu (%.1f lanes), shade %llu "
                     "(%.1f wanting, %.1f traversing)\n",
                     c[6], c[6] ? (double)c[7] / c[6] : 0.0, c[8], c[8] ? (double)c[9] / c[8] : 0.0,
                     c[10], c[10] ? (double)c[11] / c[10] : 0.0, c[10] ? (double)c[12] / c[10] : 0.0);
+#endif
     } else if (rowspec) {
         s.extend_ms = ms;
         s.extend_rays = c[3];

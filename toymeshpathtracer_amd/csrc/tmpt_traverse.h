@@ -1,6 +1,8 @@
-// tmpt_traverse.h -- LBVH2 traversal for gfx950: closest hit (Scene::HitScene,
+// tmpt_traverse.h -- BVH4Q traversal for gfx950: closest hit (Scene::HitScene,
 // scene.cpp:128-140) and any hit (the shadow query of Scatter, main.cpp:57-60,
-// whose only consumer is the hit/miss bit).
+// whose only consumer is the hit/miss bit).  Every engine (persistent path
+// kernel, wavefront, megakernel, batched HitScene) steps the same function,
+// trav_step4q2_mixed.
 //
 // * Scene query contract: result = the reference's closest hit over
 //   all triangles with strict '<', i.e. ties go to the lowest triangle index.
@@ -10,8 +12,8 @@
 // * Stack: the first SL entries of each lane live in LDS (layout [depth][lane],
 //   so a wave's accesses to one depth hit 64 distinct banks); deeper entries
 //   spill to a per-lane global area (never more than kStackTotal in all).
-// * Slab test in fma form t = b*inv - o*inv (not bit-exact, only conservative,
-//   which is all culling needs), min3/max3 reductions.
+// * Slab test in fma form t = q*(2^e/d) + (origin*inv - o*inv) (not bit-exact,
+//   only conservative, which is all culling needs).
 #pragma once
 
 #include "tmpt_internal.h"
@@ -32,7 +34,7 @@ struct TravRay {
     f3 o, d;
     float ix, iy, iz;  // 1/d (finite)
     float ox, oy, oz;  // o * inv
-    uint32_t offx, offy, offz;  // BVH4F byte offset of the near plane per axis (far = ^16)
+    uint32_t offx, offy, offz;  // octant: near plane per axis (16 / 48 / 80 = the hi plane)
 };
 
 __device__ __forceinline__ TravRay make_trav_ray(f3 o, f3 d)
@@ -53,20 +55,11 @@ __device__ __forceinline__ TravRay make_trav_ray(f3 o, f3 d)
     return r;
 }
 
-__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
-__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
-
-// entry distance of a box, or +inf-like rejection via the returned flag
-__device__ __forceinline__ bool slab(const TravRay& r, float lx, float ly, float lz, float hx,
-                                     float hy, float hz, float tlo, float tmax, float& tnear)
+// x * 2^e for the signed exponent byte e at bit `sh` of w: v_bfe_i32 + v_ldexp_f32,
+// exact (a power-of-two scaling, no under/overflow for the 1/d of a unit direction)
+__device__ __forceinline__ float exp_mul(float x, uint32_t w, int sh)
 {
-    float t0x = __builtin_fmaf(lx, r.ix, -r.ox), t1x = __builtin_fmaf(hx, r.ix, -r.ox);
-    float t0y = __builtin_fmaf(ly, r.iy, -r.oy), t1y = __builtin_fmaf(hy, r.iy, -r.oy);
-    float t0z = __builtin_fmaf(lz, r.iz, -r.oz), t1z = __builtin_fmaf(hz, r.iz, -r.oz);
-    float tn = max3f(fminf(t0x, t1x), fminf(t0y, t1y), fmaxf(fminf(t0z, t1z), tlo));
-    float tf = min3f(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fminf(fmaxf(t0z, t1z), tmax));
-    tnear = tn;
-    return tn <= tf * kTfarSlack;
+    return __builtin_amdgcn_ldexpf(x, (int)__builtin_amdgcn_sbfe(w, sh, 8));
 }
 
 // Pins a loaded triangle record's used words in registers at this point (no
@@ -78,6 +71,7 @@ __device__ __forceinline__ void materialize(float4& a, float4& b, float4& c)
                  "+v"(b.w), "+v"(c.x), "+v"(c.y));
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
@@ -92,7 +86,7 @@ template <int BLOCK, int SL>
 struct TravStack {
     lds_u32* lds;    // &s_stack[threadIdx.x]; entry k at lds[k * BLOCK]
     uint32_t* glob;  // kStackTotal - SL entries of this lane
-    const lds_u4* top = nullptr;  // LDS copy of BVH4 nodes [0, ntop) (FMT 4), 4 uint4 each
+    const lds_u4* top = nullptr;  // LDS copy of BVH4 nodes [0, ntop) (TOPC steps), 4 uint4 each
     uint32_t ntop = 0;
     __device__ __forceinline__ TravStack(uint32_t* l, uint32_t* g) : lds((lds_u32*)l), glob(g) {}
     __device__ __forceinline__ void push(int& sp, int v)
@@ -131,13 +125,10 @@ struct TravStack {
 };
 
 struct SceneView {
-    const BvhNode* __restrict__ nodes;
     const Bvh4Node* __restrict__ nodes4;
-    const char* __restrict__ nodes4f;  // Bvh4FNode array, addressed by byte offset
     const TriPre* __restrict__ tri_pre;
     const TriOrig* __restrict__ tri_orig;
     int32_t n;
-    ShadowGrid sg;  // by value: axes, origin, scale, device arrays (R = 0: none)
     int32_t n_nodes4 = 0;
 };
 
@@ -162,345 +153,27 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
     ts.bu = ts.bv = 0.0f;
 }
 
-// One traversal step: one internal node (both child boxes) or one leaf
-// triangle.  Returns true when the query is finished (stack empty, or the
-// first accepted hit of an any-hit query).
-template <bool ANY, bool COUNT, int BLOCK, int SL>
-__device__ __forceinline__ bool trav_step(const SceneView& sv, const TravRay& r, float tlo,
-                                          float tmin, float tmax, TravState& ts,
-                                          TravStack<BLOCK, SL>& st, TravCount& cnt)
-{
-    if (ts.node >= 0) {
-        const float4* p = reinterpret_cast<const float4*>(sv.nodes + ts.node);
-        float4 a = p[0], b = p[1], c = p[2];
-        int4 lk = reinterpret_cast<const int4*>(p)[3];
-        if (COUNT) ++cnt.nodes;
-        float tn0, tn1;
-        bool h0 = slab(r, a.x, a.y, a.z, a.w, b.x, b.y, tlo, ts.bt, tn0);
-        bool h1 = slab(r, b.z, b.w, c.x, c.y, c.z, c.w, tlo, ts.bt, tn1);
-        if (h0 && h1) {
-            int nearc = lk.x, farc = lk.y;
-            if (tn1 < tn0) { nearc = lk.y; farc = lk.x; }
-            st.push(ts.sp, farc);
-            ts.node = nearc;
-            return false;
-        }
-        if (h0 || h1) {
-            ts.node = h0 ? lk.x : lk.y;
-            return false;
-        }
-    } else {
-        const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + (~ts.node));
-        float4 a = p[0], b = p[1], c = p[2];
-        if (COUNT) ++cnt.tris;
-        float t, u, v;
-        if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
-                    t, u, v)) {
-            int id = __float_as_int(c.y);
-            if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
-                ts.bt = t;
-                ts.bu = u;
-                ts.bv = v;
-                ts.best = id;
-                if (ANY) return true;
-            }
-        }
-    }
-    if (ts.sp == 0) return true;
-    ts.node = st.pop(ts.sp);
-    return false;
-}
-
-// 2^e for the signed exponent byte e of a BVH4Q node (bits 0-7 of `b`)
-__device__ __forceinline__ float exp_scale(uint32_t b) { return __uint_as_float((uint32_t)((int)(int8_t)(b & 0xFFu) + 127) << 23); }
-// x * 2^e for the signed exponent byte e at bit `sh` of w: v_bfe_i32 + v_ldexp_f32,
-// exact (a power-of-two scaling, no under/overflow for the 1/d of a unit direction)
-__device__ __forceinline__ float exp_mul(float x, uint32_t w, int sh)
-{
-    return __builtin_amdgcn_ldexpf(x, (int)__builtin_amdgcn_sbfe(w, sh, 8));
-}
-
-template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool leaf_tris(const SceneView& sv, const TravRay& r, float tmin,
-                                          float tmax, TravState& ts, uint32_t code,
-                                          TravCount& cnt)
-{
-    const uint32_t first = code & kLeafFirstMask;
-    const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
-    for (uint32_t k = 0; k < n; ++k) {
-        const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
-        float4 a = p[0], b = p[1], c = p[2];
-        if (COUNT) ++cnt.tris;
-        float t, u, v;
-        if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
-                    t, u, v)) {
-            int id = __float_as_int(c.y);
-            if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
-                ts.bt = t;
-                ts.bu = u;
-                ts.bv = v;
-                ts.best = id;
-                if (ANY) return true;
-            }
-        }
-    }
-    return false;
-}
-
-// One step over the 4-wide quantised BVH: one node (four child boxes decoded
-// as origin + q*2^e, slab distances t = q*(2^e/d) + (origin-o)/d, one fma per
-// plane) or one leaf (its triangle range).  Closest hit: hit children sorted
-// near to far (5-exchange network), nearest taken, others pushed far first.
-template <bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
-__device__ __forceinline__ bool trav_step4(const SceneView& sv, const TravRay& r, float tlo,
-                                           float tmin, float tmax, TravState& ts,
-                                           TravStack<BLOCK, SL>& st, TravCount& cnt)
-{
-    if (ts.node >= 0) {
-        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
-        uint4 A = p[0], B = p[1], C = p[2];
-        int4 L = reinterpret_cast<const int4*>(p)[3];
-        if (COUNT) ++cnt.nodes;
-        const float ax = exp_scale(A.w) * r.ix, bx = (__uint_as_float(A.x) - r.o.x) * r.ix;
-        const float ay = exp_scale(A.w >> 8) * r.iy, by = (__uint_as_float(A.y) - r.o.y) * r.iy;
-        const float az = exp_scale(A.w >> 16) * r.iz, bz = (__uint_as_float(A.z) - r.o.z) * r.iz;
-        const uint32_t mask = A.w >> 24;
-        float key[4];
-        int ch[4] = {L.x, L.y, L.z, L.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int sh = 8 * k;
-            float t0x = __builtin_fmaf((float)((B.x >> sh) & 255u), ax, bx);
-            float t1x = __builtin_fmaf((float)((B.y >> sh) & 255u), ax, bx);
-            float t0y = __builtin_fmaf((float)((B.z >> sh) & 255u), ay, by);
-            float t1y = __builtin_fmaf((float)((B.w >> sh) & 255u), ay, by);
-            float t0z = __builtin_fmaf((float)((C.x >> sh) & 255u), az, bz);
-            float t1z = __builtin_fmaf((float)((C.y >> sh) & 255u), az, bz);
-            float tn = max3f(fminf(t0x, t1x), fminf(t0y, t1y), fmaxf(fminf(t0z, t1z), tlo));
-            float tf = min3f(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fminf(fmaxf(t0z, t1z), ts.bt));
-            bool hit = ((mask >> k) & 1u) && tn <= tf * kTfarSlack;
-            key[k] = hit ? tn : INFINITY;
-        }
-        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
-                 (key[3] != INFINITY);
-        if (nh > 0) {
-            if (SORT) {
-#define TMPT_CSWAP(i, j)                                            \
-    if (key[j] < key[i]) {                                          \
-        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
-        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
-    }
-                TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
-#undef TMPT_CSWAP
-                // hits now occupy 0..nh-1, nearest first
-                if (nh > 3) st.push(ts.sp, ch[3]);
-                if (nh > 2) st.push(ts.sp, ch[2]);
-                if (nh > 1) st.push(ts.sp, ch[1]);
-                ts.node = ch[0];
-            } else {
-                int next = 0;
-                bool have = false;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (key[k] != INFINITY) {
-                        if (!have) {
-                            next = ch[k];
-                            have = true;
-                        } else {
-                            st.push(ts.sp, ch[k]);
-                        }
-                    }
-                }
-                ts.node = next;
-            }
-            return false;
-        }
-    } else {
-        if (leaf_tris<ANY, COUNT>(sv, r, tmin, tmax, ts, (uint32_t)ts.node, cnt)) return true;
-    }
-    if (ts.sp == 0) return true;
-    ts.node = st.pop(ts.sp);
-    return false;
-}
-
-// Same step with the query kind chosen per lane at run time (the persistent
-// path engine mixes closest-hit and shadow queries in one wave): children are
-// always visited near to far; a shadow query stops at its first accepted hit.
-template <bool COUNT, int BLOCK, int SL>
-__device__ __forceinline__ bool trav_step4_mixed(const SceneView& sv, const TravRay& r, bool any,
-                                                 TravState& ts, TravStack<BLOCK, SL>& st,
-                                                 TravCount& cnt)
-{
-    if (ts.node >= 0) {
-        const uint4* p = reinterpret_cast<const uint4*>(sv.nodes4 + ts.node);
-        uint4 A = p[0], B = p[1], C = p[2];
-        int4 L = reinterpret_cast<const int4*>(p)[3];
-        if (COUNT) ++cnt.nodes;
-        const float ax = exp_scale(A.w) * r.ix, bx = (__uint_as_float(A.x) - r.o.x) * r.ix;
-        const float ay = exp_scale(A.w >> 8) * r.iy, by = (__uint_as_float(A.y) - r.o.y) * r.iy;
-        const float az = exp_scale(A.w >> 16) * r.iz, bz = (__uint_as_float(A.z) - r.o.z) * r.iz;
-        const uint32_t mask = A.w >> 24;
-        float key[4];
-        int ch[4] = {L.x, L.y, L.z, L.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int sh = 8 * k;
-            float t0x = __builtin_fmaf((float)((B.x >> sh) & 255u), ax, bx);
-            float t1x = __builtin_fmaf((float)((B.y >> sh) & 255u), ax, bx);
-            float t0y = __builtin_fmaf((float)((B.z >> sh) & 255u), ay, by);
-            float t1y = __builtin_fmaf((float)((B.w >> sh) & 255u), ay, by);
-            float t0z = __builtin_fmaf((float)((C.x >> sh) & 255u), az, bz);
-            float t1z = __builtin_fmaf((float)((C.y >> sh) & 255u), az, bz);
-            float tn = max3f(fminf(t0x, t1x), fminf(t0y, t1y), fmaxf(fminf(t0z, t1z), 0.0f));
-            float tf = min3f(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fminf(fmaxf(t0z, t1z), ts.bt));
-            bool hit = ((mask >> k) & 1u) && tn <= tf * kTfarSlack;
-            key[k] = hit ? tn : INFINITY;
-        }
-        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
-                 (key[3] != INFINITY);
-        if (nh > 0) {
-#define TMPT_CSWAP(i, j)                                            \
-    if (key[j] < key[i]) {                                          \
-        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
-        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
-    }
-            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
-#undef TMPT_CSWAP
-            if (nh > 3) st.push(ts.sp, ch[3]);
-            if (nh > 2) st.push(ts.sp, ch[2]);
-            if (nh > 1) st.push(ts.sp, ch[1]);
-            ts.node = ch[0];
-            return false;
-        }
-    } else {
-        const uint32_t code = (uint32_t)ts.node;
-        const uint32_t first = code & kLeafFirstMask;
-        const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
-        for (uint32_t k = 0; k < n; ++k) {
-            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
-            float4 a = p[0], b = p[1], c = p[2];
-            if (COUNT) ++cnt.tris;
-            float t, u, v;
-            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
-                        t, u, v)) {
-                int id = __float_as_int(c.y);
-                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
-                    ts.bt = t;
-                    ts.bu = u;
-                    ts.bv = v;
-                    ts.best = id;
-                    if (any) return true;
-                }
-            }
-        }
-    }
-    if (ts.sp == 0) return true;
-    ts.node = st.pop(ts.sp);
-    return false;
-}
-
-typedef float v2f __attribute__((ext_vector_type(2)));
-
-// One step over BVH4F (f32 child boxes): near/far planes chosen by the ray's
-// octant (byte offsets), slab distances by packed fma over child pairs, so a
-// node costs 12 v_pk_fma + 4 compares per child instead of per-child unpacking
-// and min/max.  The same children, links, order and leaf handling as
-// trav_step4_mixed; boxes are the unquantised padded boxes (tighter).
-template <bool COUNT, int BLOCK, int SL>
-__device__ __forceinline__ bool trav_step4f_mixed(const SceneView& sv, const TravRay& r, bool any,
-                                                  TravState& ts, TravStack<BLOCK, SL>& st,
-                                                  TravCount& cnt)
-{
-    if (ts.node >= 0) {
-        const uint32_t nb = (uint32_t)ts.node << 7;
-        const char* base = sv.nodes4f;
-        const float4 nx = *reinterpret_cast<const float4*>(base + (nb | r.offx));
-        const float4 fx = *reinterpret_cast<const float4*>(base + (nb | (r.offx ^ 16u)));
-        const float4 ny = *reinterpret_cast<const float4*>(base + (nb | r.offy));
-        const float4 fy = *reinterpret_cast<const float4*>(base + (nb | (r.offy ^ 16u)));
-        const float4 nz = *reinterpret_cast<const float4*>(base + (nb | r.offz));
-        const float4 fz = *reinterpret_cast<const float4*>(base + (nb | (r.offz ^ 16u)));
-        const int4 L = *reinterpret_cast<const int4*>(base + (nb | 96u));
-        if (COUNT) ++cnt.nodes;
-        const v2f ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
-        const v2f ox = {-r.ox, -r.ox}, oy = {-r.oy, -r.oy}, oz = {-r.oz, -r.oz};
-#define TMPT_PL(V, I, O, lo2, hi2)                                                   \
-        const v2f lo2 = __builtin_elementwise_fma((v2f){V.x, V.y}, I, O);               \
-        const v2f hi2 = __builtin_elementwise_fma((v2f){V.z, V.w}, I, O);
-        TMPT_PL(nx, ix, ox, nx01, nx23)
-        TMPT_PL(fx, ix, ox, fx01, fx23)
-        TMPT_PL(ny, iy, oy, ny01, ny23)
-        TMPT_PL(fy, iy, oy, fy01, fy23)
-        TMPT_PL(nz, iz, oz, nz01, nz23)
-        TMPT_PL(fz, iz, oz, fz01, fz23)
-#undef TMPT_PL
-        const float tnear[4] = {nx01.x, nx01.y, nx23.x, nx23.y};
-        const float tnear_y[4] = {ny01.x, ny01.y, ny23.x, ny23.y};
-        const float tnear_z[4] = {nz01.x, nz01.y, nz23.x, nz23.y};
-        const float tfar[4] = {fx01.x, fx01.y, fx23.x, fx23.y};
-        const float tfar_y[4] = {fy01.x, fy01.y, fy23.x, fy23.y};
-        const float tfar_z[4] = {fz01.x, fz01.y, fz23.x, fz23.y};
-        float key[4];
-        int ch[4] = {L.x, L.y, L.z, L.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float tn = fmaxf(fmaxf(tnear[k], tnear_y[k]), fmaxf(tnear_z[k], 0.0f));
-            float tf = fminf(fminf(tfar[k], tfar_y[k]), fminf(tfar_z[k], ts.bt));
-            key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
-        }
-        int nh = (key[0] != INFINITY) + (key[1] != INFINITY) + (key[2] != INFINITY) +
-                 (key[3] != INFINITY);
-        if (nh > 0) {
-#define TMPT_CSWAP(i, j)                                            \
-    if (key[j] < key[i]) {                                          \
-        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
-        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
-    }
-            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
-#undef TMPT_CSWAP
-            if (nh > 3) st.push(ts.sp, ch[3]);
-            if (nh > 2) st.push(ts.sp, ch[2]);
-            if (nh > 1) st.push(ts.sp, ch[1]);
-            ts.node = ch[0];
-            return false;
-        }
-    } else {
-        const uint32_t code = (uint32_t)ts.node;
-        const uint32_t first = code & kLeafFirstMask;
-        const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
-        for (uint32_t k = 0; k < n; ++k) {
-            const float4* p = reinterpret_cast<const float4*>(sv.tri_pre + first + k);
-            float4 a = p[0], b = p[1], c = p[2];
-            if (COUNT) ++cnt.tris;
-            float t, u, v;
-            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
-                        t, u, v)) {
-                int id = __float_as_int(c.y);
-                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
-                    ts.bt = t;
-                    ts.bu = u;
-                    ts.bv = v;
-                    ts.best = id;
-                    if (any) return true;
-                }
-            }
-        }
-    }
-    if (ts.sp == 0) return true;
-    ts.node = st.pop(ts.sp);
-    return false;
-}
-
-// One step over BVH4Q (64-B quantised nodes) with the BVH4F step's decoding:
-// near/far byte planes picked per axis by the ray's octant (one v_cndmask per
-// plane dword), t = q * (2^e/d) + fma(origin, 1/d, -o/d) by packed fma over
-// child pairs, no per-child min/max and no mask test (empty slots carry an
-// inverted box and link to the null leaf).  4 loads per node (the TA cost of a
-// divergent gather scales with bytes per lane) at ~BVH4F's VALU count.
-template <bool COUNT, int BLOCK, int SL, int SORTK = 0, bool TOPC = false, int KIND = 0>
+// One step over BVH4Q (64-B quantised nodes): one node or one leaf.
+// Node: near/far byte planes picked per axis by the ray's octant (one
+// v_cndmask per plane dword), t = q * (2^e/d) + fma(origin, 1/d, -o/d) by
+// packed fma over child pairs, no per-child min/max and no mask test (empty
+// slots carry an inverted box and link to the null leaf); the nearest hit
+// child is next, the others are pushed pairwise-ordered.  Leaf: its triangles'
+// Moller-Trumbore tests (bit-exact, maths.cpp:339-380) with t in [tmin, tmax];
+// ties on t go to the lowest triangle index.  `any` (run time): stop at the
+// first accepted triangle (the shadow query).  Returns true when the query is
+// finished; ts.node is undefined after that (the next query re-inits it).
+// tlo: lower clamp of a box's entry distance, min(tmin, 0) (boxes behind the
+// origin hold no t >= 0 hit); the path engines pass the reference's constant
+// range kMinT..kMaxT (main.cpp:30-31), the batched HitScene any per-ray range.
+// KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a voted
+// round), so the other kind's code is not emitted.  TOPC: node indices below
+// st.ntop are read from the block's LDS copy of the top levels.
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
-                                                   TravCount& cnt)
+                                                   TravCount& cnt, float tlo = 0.0f, float tmin = kMinT,
+                                                   float tmax = kMaxT)
 {
     // KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a
     // voted round), so the other kind's code is not emitted at all
@@ -554,26 +227,11 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         int ch[4] = {L.x, L.y, L.z, L.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            float tn = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], 0.0f));
+            float tn = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], tlo));
             float tf = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], ts.bt));
             key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
         }
-        if (SORTK == 0) {  // all hit children near to far (misses sort last as +inf)
-#define TMPT_CSWAP(i, j)                                            \
-    if (key[j] < key[i]) {                                          \
-        float tk = key[i]; key[i] = key[j]; key[j] = tk;             \
-        int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;                   \
-    }
-            TMPT_CSWAP(0, 1) TMPT_CSWAP(2, 3) TMPT_CSWAP(0, 2) TMPT_CSWAP(1, 3) TMPT_CSWAP(1, 2)
-#undef TMPT_CSWAP
-            if (key[0] != INFINITY) {
-                if (key[3] != INFINITY) st.push(ts.sp, ch[3]);
-                if (key[2] != INFINITY) st.push(ts.sp, ch[2]);
-                if (key[1] != INFINITY) st.push(ts.sp, ch[1]);
-                ts.node = ch[0];
-                return false;
-            }
-        } else {  // nearest child next; the others pushed pairwise-ordered only
+        {  // nearest child next; the others pushed pairwise-ordered only
             const bool s01 = key[1] < key[0], s23 = key[3] < key[2];
             const float ka = s01 ? key[1] : key[0], kao = s01 ? key[0] : key[1];
             const int ca = s01 ? ch[1] : ch[0], cao = s01 ? ch[0] : ch[1];
@@ -598,7 +256,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         auto tri = [&](const float4& a, const float4& b, const float4& c) -> bool {
             if (COUNT) ++cnt.tris;
             float t, u, v;
-            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), kMinT, kMaxT,
+            if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
                         t, u, v)) {
                 int id = __float_as_int(c.y);
                 if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
@@ -629,9 +287,9 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             float t0, u0, w0, t1, u1, w1;
             if (COUNT) cnt.tris += n > 1u ? 2u : 1u;
             const bool ok0 = mt_test_flat(r.o, r.d, mk(a0.x, a0.y, a0.z), mk(a0.w, b0.x, b0.y),
-                                          mk(b0.z, b0.w, c0.x), kMinT, kMaxT, t0, u0, w0);
+                                          mk(b0.z, b0.w, c0.x), tmin, tmax, t0, u0, w0);
             const bool ok1 = mt_test_flat(r.o, r.d, mk(a1.x, a1.y, a1.z), mk(a1.w, b1.x, b1.y),
-                                          mk(b1.z, b1.w, c1.x), kMinT, kMaxT, t1, u1, w1) &&
+                                          mk(b1.z, b1.w, c1.x), tmin, tmax, t1, u1, w1) &&
                              n > 1u;
             const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
             const bool acc0 = ok0 && (t0 < ts.bt || (t0 == ts.bt && ts.best >= 0 && id0 < ts.best));
@@ -667,28 +325,6 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
     return false;
 }
 
-// node format of the persistent engine: 0 = BVH4Q (mask + min/max decode),
-// 1 = BVH4F (f32 boxes), 2 = BVH4Q with octant decode
-template <int FMT, bool COUNT, int BLOCK, int SL>
-__device__ __forceinline__ bool trav_step_fmt(const SceneView& sv, const TravRay& r, bool any,
-                                              TravState& ts, TravStack<BLOCK, SL>& st, TravCount& cnt)
-{
-    if (FMT == 1) return trav_step4f_mixed<COUNT>(sv, r, any, ts, st, cnt);
-    if (FMT == 2) return trav_step4q2_mixed<COUNT, BLOCK, SL, 0>(sv, r, any, ts, st, cnt);
-    if (FMT == 3) return trav_step4q2_mixed<COUNT, BLOCK, SL, 1>(sv, r, any, ts, st, cnt);
-    if (FMT == 4) return trav_step4q2_mixed<COUNT, BLOCK, SL, 1, true>(sv, r, any, ts, st, cnt);
-    return trav_step4_mixed<COUNT>(sv, r, any, ts, st, cnt);
-}
-
-template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL, bool SORT = !ANY>
-__device__ __forceinline__ bool trav_step_w(const SceneView& sv, const TravRay& r, float tlo,
-                                            float tmin, float tmax, TravState& ts,
-                                            TravStack<BLOCK, SL>& st, TravCount& cnt)
-{
-    if (WIDE) return trav_step4<ANY, COUNT, BLOCK, SL, SORT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
-    return trav_step<ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt);
-}
-
 // A ray with a NaN in its origin or direction can never be accepted by
 // Moller-Trumbore (det, u, v and t all become NaN and every comparison of
 // maths.cpp:345-371 is false), so the reference's HitScene returns -1 for it.
@@ -702,56 +338,10 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
            __builtin_isnan(d.y) | __builtin_isnan(d.z);
 }
 
-// Shadow query through the light-space grid (tmpt_shadow.hip): is some
-// triangle hit by (p, light_dir()) with t in [kMinT, kMaxT]?  One cell, a
-// binary search past the triangles that end below p along L, then the
-// bit-exact Moller-Trumbore test in order until one accepts.  Returns the
-// original triangle index of that hit or -1 (t, u, v of the hit).
-__device__ __forceinline__ int shadow_grid_hit(const SceneView& sv, f3 p, f3 ldir, float& t, float& u,
-                                               float& v)
-{
-    const ShadowGrid& g = sv.sg;
-    const float pu = p.x * g.U[0] + p.y * g.U[1] + p.z * g.U[2];
-    const float pv = p.x * g.V[0] + p.y * g.V[1] + p.z * g.V[2];
-    const float fu = (pu - g.u0) * g.inv_cu, fv = (pv - g.v0) * g.inv_cv;
-    // outside the padded projection of every triangle (or NaN): nothing to hit
-    if (!(fu >= 0.0f && fu < (float)g.R && fv >= 0.0f && fv < (float)g.R)) return -1;
-    const uint32_t c = (uint32_t)(int)fv * (uint32_t)g.R + (uint32_t)(int)fu;
-    uint32_t lo = g.start[c];
-    const uint32_t end = g.start[c + 1];
-    // a hit at t >= kMinT reaches dot(p, L) + kMinT up L; the margin covers
-    // float rounding of dot(p, L) and of Moller-Trumbore's t
-    const float dl = p.x * ldir.x + p.y * ldir.y + p.z * ldir.z;
-    const float thr = dl + kMinT - 1e-4f * (1.0f + fabsf(dl));
-    uint32_t hi = end;
-    while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (g.tmax[m] < thr) lo = m + 1;
-        else hi = m;
-    }
-    for (uint32_t k = lo; k < end; ++k) {
-        const float4* q = reinterpret_cast<const float4*>(sv.tri_pre + g.slot[k]);
-        const float4 a = q[0], b = q[1], cc = q[2];
-        if (mt_test(p, ldir, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, cc.x), kMinT, kMaxT, t, u, v))
-            return __float_as_int(cc.y);
-    }
-    return -1;
-}
-
-// The shadow-grid cell of a shadow ray's origin as a tri_pre range
-// {first, count} (count 0: no triangle can be hit).
-__device__ __forceinline__ uint2 shadow_grid_cell(const SceneView& sv, f3 p)
-{
-    const ShadowGrid& g = sv.sg;
-    const float pu = p.x * g.U[0] + p.y * g.U[1] + p.z * g.U[2];
-    const float pv = p.x * g.V[0] + p.y * g.V[1] + p.z * g.V[2];
-    const float fu = (pu - g.u0) * g.inv_cu, fv = (pv - g.v0) * g.inv_cv;
-    if (!(fu >= 0.0f && fu < (float)g.R && fv >= 0.0f && fv < (float)g.R)) return make_uint2(0u, 0u);
-    return g.cell[(uint32_t)(int)fv * (uint32_t)g.R + (uint32_t)(int)fu];
-}
-
-// Whole query in one call.  Returns the original triangle index or -1.
-template <bool WIDE, bool ANY, bool COUNT, int BLOCK, int SL>
+// Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:129-140).
+// Returns the original triangle index or -1; (bt, bu, bv) of the hit.  TOPC:
+// the caller's block holds the top BVH levels in LDS (st.top).
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
                                         float tmax, float& bt, float& bu, float& bv,
                                         TravStack<BLOCK, SL>& st, TravCount& cnt)
@@ -760,7 +350,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
     trav_init(ts, tmax);
     if (sv.n > 0 && !ray_has_nan(r.o, r.d)) {
         const float tlo = fminf(tmin, 0.0f);
-        while (!trav_step_w<WIDE, ANY, COUNT>(sv, r, tlo, tmin, tmax, ts, st, cnt)) {
+        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
     }
     bt = ts.bt;
