@@ -332,6 +332,7 @@ int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const cha
     TMPT_GUARD_BEGIN
     if (!out || n < 0 || (n > 0 && !tris)) return bad("tmpt_scene_create: bad arguments");
     *out = nullptr;
+    (void)hipGetLastError();  // a failed call before this one must not fail the build's checks
     Options opt;
     if (int rc = options_parse(opt, options, true)) {
         set_error(std::string("tmpt_scene_create: ") + last_error());
@@ -511,6 +512,7 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     const bool progressive = d->spp_begin > 0 || (d->spp_count > 0 && d->spp_count < d->spp);
     if (progressive && (d->engine != TMPT_ENGINE_PERSISTENT || d->seed_mode != TMPT_SEED_PIXEL))
         return bad("tmpt_render: progressive spp needs the persistent engine and pixel seeding");
+    (void)hipGetLastError();  // clear a stale error of an earlier failed call (launch checks read it)
     Scene& s = h->s;
     TMPT_HIP(hipSetDevice(s.device));
     const int32_t rows = tmpt_tile_rows(d);
@@ -561,24 +563,29 @@ int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, cons
     uint32_t* d_frame = nullptr;
     uint64_t* d_total = nullptr;
     std::vector<ncclComm_t> comms;
-    auto cleanup = [&]() {
-        for (int g = 0; g < nd; ++g) {
-            (void)hipSetDevice(devices[g]);
-            if (streams[(size_t)g]) (void)hipStreamSynchronize(streams[(size_t)g]);
-        }
+    auto cleanup = [&]() {  // touches only devices whose resources exist (a bad ordinal is never set)
+        for (int g = 0; g < nd; ++g)
+            if (streams[(size_t)g]) {
+                (void)hipSetDevice(devices[g]);
+                (void)hipStreamSynchronize(streams[(size_t)g]);
+            }
         for (ncclComm_t c : comms)
             if (c) (void)rccl().comm_destroy(c);
         for (int g = 0; g < nd; ++g) {
+            if (!streams[(size_t)g] && !d_tile[(size_t)g] && !d_rays[(size_t)g]) continue;
             (void)hipSetDevice(devices[g]);
             if (d_tile[(size_t)g]) (void)hipFree(d_tile[(size_t)g]);
             if (d_rays[(size_t)g]) (void)hipFree(d_rays[(size_t)g]);
             if (streams[(size_t)g]) (void)hipStreamDestroy(streams[(size_t)g]);
         }
-        (void)hipSetDevice(devices[0]);
-        if (d_gather) (void)hipFree(d_gather);
-        if (d_frame) (void)hipFree(d_frame);
-        if (d_total) (void)hipFree(d_total);
+        if (d_gather || d_frame || d_total) {
+            (void)hipSetDevice(devices[0]);
+            if (d_gather) (void)hipFree(d_gather);
+            if (d_frame) (void)hipFree(d_frame);
+            if (d_total) (void)hipFree(d_total);
+        }
         for (auto* sc : scenes) tmpt_scene_destroy(sc);
+        (void)hipGetLastError();  // leave no sticky error behind for this thread's next call
     };
     auto fail = [&](const std::string& msg, int rc) {
         cleanup();
