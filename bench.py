@@ -22,11 +22,14 @@ oracle legs (tests/); the line also reports the other modes' throughput
 (seed_modes), timed the same way after the main run.
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
-  roofline      dominant kernel (k_path: all queries of the frame): algorithmic
-                bytes per launch (B_ray = 32 + 16 + 64*N_node +
-                36*N_tri, N_node/N_tri measured by an instrumented run of the same
-                kernel on the same frame at reduced spp) / its mean launch time,
-                HIP-event timed on the stream the kernel runs on; peak 8 TB/s
+  roofline      dominant kernel (k_path: all queries of the frame), its mean
+                launch time HIP-event timed on the stream it runs on, against
+                three counter-backed ceilings (VALU issue, L2 requests, HBM
+                bytes; per-query counts from the committed rocprofv3 record
+                profiles/r*_counters_k_path.json); `bound` = the highest.  The
+                SURVEY.md §8d algorithmic bytes (B_ray = 32 + 16 + 64*N_node +
+                36*N_tri, N_node/N_tri from an instrumented run of the same kernel
+                at reduced spp) are reported under roofline.algorithmic
   cpu_baseline  the CPU restatement of the reference algorithm (octree +
                 Moller-Trumbore, oracle/, bit-exact to the reference binary on the
                 pinned cases) timed on this host on a bounded row sample of the same
@@ -55,6 +58,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "MRays/s on sponza.obj 1920x1080 64spp at 1/2/4/8 GPUs; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+L2_PEAK_BPS = 34.5e12  # MI355X_MICROARCH.md, L2 (aggregate over the 8 XCDs)
 BAND_ROWS = 1   # rows dealt round-robin: every rank gets H/N rows of statistically equal cost
 S_NODE = 64            # bytes per visited node: BVH4Q (4 quantised child boxes + links) or BVH2
 S_TRI = 36             # bytes per triangle test (3 x vec3), SURVEY.md §8d
@@ -94,20 +98,72 @@ def scene_path(obj: str) -> str:
     return os.path.join(ROOT, "data", obj)
 
 
-def pmc_traffic() -> dict:
-    """HBM bytes per k_path launch from the newest committed PMC pass
-    (profiles/r*_pmc_k_path.json, written by tools/prof_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench; FETCH_SIZE x2 per
-    MI355X_MICROARCH.md).  PMC needs rocprofv3 around the process, so the live
-    bench cannot collect it itself; null when no profile is present."""
+def counter_record() -> dict:
+    """The newest counter record of k_path (profiles/r*_counters_k_path.json,
+    tools/roofline_counters.py over rocprofv3 --pmc passes of this bench, one
+    pass per counter set, and the calibration kernel tools/pmc_calib.hip).
+    PMC needs rocprofv3 around the process, so the live bench cannot collect
+    it itself; it scales the record's per-query figures by its own queries and
+    launch time.  stale = the record was taken with another libtmpt.so build."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_k_path.json")))
+    import hashlib
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_counters_k_path.json")))
     if not files:
-        return {"traffic": None}
+        return {}
     with open(files[-1]) as f:
         rec = json.load(f)
-    return {"traffic": round(rec["hbm_bytes_per_launch"]), "traffic_unit": "bytes/launch",
-            "traffic_source": os.path.relpath(files[-1], ROOT), "traffic_kernel": rec["kernel"]}
+    rec["_source"] = os.path.relpath(files[-1], ROOT)
+    try:
+        with open(tm.lib_path, "rb") as f:
+            rec["_stale"] = hashlib.sha256(f.read()).hexdigest()[:16] != rec.get("lib_sha256_16")
+    except OSError:
+        rec["_stale"] = None
+    return rec
+
+
+def roofline(queries: float, launch_ms: float, b_ray: float, kernel: str) -> dict:
+    """Ceilings of the dominant kernel, each as achieved / peak over the live
+    launch time (the bound is the resource that binds, from
+    counters; the SURVEY §8d algorithmic bytes are reported beside it):
+      valu_issue  VALU instructions (per query, counted) / (1024 SIMDs x 2.4 GHz / 2)
+      l2          L1->L2 requests x 128 B (per query, counted) / 34.5 TB/s
+      hbm         fabric bytes (EA requests by size, counted) / 8 TB/s
+    `bound` is the highest; `achieved`, `peak`, `frac` are its.  The algorithmic
+    bytes (48 + 64 N_node + 36 N_tri per query, instrumented run) are served by
+    L1 / L2 (hit rates in the record), so against HBM they are not a bound."""
+    t = launch_ms * 1e-3
+    rec = counter_record()
+    alg = {"bytes_per_query": round(b_ray, 1), "tbps": round(b_ray * queries / t / 1e12, 3),
+           "frac_of_l2_peak": round(b_ray * queries / t / L2_PEAK_BPS, 4),
+           "frac_of_hbm_peak": round(b_ray * queries / t / (HBM_PEAK_GBS * 1e9), 4),
+           "note": "SURVEY.md 8d algorithmic bytes; served from L1/L2 (see l2.hit_rate), not HBM"}
+    out = {"kernel": kernel, "avg_launch_ms": round(launch_ms, 4), "queries_per_launch": int(queries),
+           "algorithmic": alg}
+    if not rec:
+        out.update({"bound": "hbm", "achieved": round(alg["tbps"] * 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": alg["frac_of_hbm_peak"], "traffic": None})
+        return out
+    pq = rec["per_query"]
+    valu_rate = pq["valu_insts"] * queries / t
+    valu_peak = 1024 * 2.4e9 / 2.0
+    l2_rate = pq["l2_bytes"] * queries / t
+    hbm_bytes = (pq["hbm_read_bytes"] + pq["hbm_write_bytes"]) * queries
+    ceil = {
+        "valu_issue": {"achieved": round(valu_rate / 1e9, 1), "peak": round(valu_peak / 1e9, 1), "unit": "Ginstr/s",
+                       "frac": round(valu_rate / valu_peak, 4),
+                       "lane_utilisation": round(rec["valu"]["lane_utilisation"], 4)},
+        "l2": {"achieved": round(l2_rate / 1e9, 1), "peak": L2_PEAK_BPS / 1e9, "unit": "GB/s",
+               "frac": round(l2_rate / L2_PEAK_BPS, 4), "hit_rate": round(rec["l2"]["hit_rate"], 4)},
+        "hbm": {"achieved": round(hbm_bytes / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hbm_bytes / t / (HBM_PEAK_GBS * 1e9), 4)},
+    }
+    bound = max(ceil, key=lambda k: ceil[k]["frac"])
+    out.update({"bound": bound, "achieved": ceil[bound]["achieved"], "peak": ceil[bound]["peak"],
+                "unit": ceil[bound]["unit"], "frac": ceil[bound]["frac"],
+                "traffic": round(hbm_bytes), "traffic_unit": "bytes/launch (HBM: EA read+write requests by size)",
+                "ceilings": ceil, "counter_source": rec["_source"], "counter_record_stale": rec["_stale"],
+                "counter_kernel": rec["kernel"].split("(")[0]})
+    return out
 
 
 def host_cpus() -> dict:
@@ -137,7 +193,7 @@ def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
     oracle/) on ALL host cores -- as many threads as the process may use, like
     TBB's default_num_threads() (main.cpp:250-251) -- timed on a bounded sample
     of the same frame: batches of rows y = o (mod S), S ~ H / (2 threads) (two rows per
-    thread), of which the pixels x = c (mod 16) (pixel and sample seeding:
+    thread), of which the pixels x = c (mod 32) (pixel and sample seeding:
     pixels are independent; row seeding renders whole rows of fewer rows per
     batch, its stream runs along the row), batches in a fixed scattered order
     until ~args.cpu_seconds have passed.  Also compares those pixels with the
@@ -148,7 +204,7 @@ def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
     osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
     seed = {"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL, "row": oracle.SEED_ROW}[args.seed_mode]
     row_mode = args.seed_mode == "row"
-    xs = 1 if row_mode else 16
+    xs = 1 if row_mode else 32
     stride = max(1, H // (16 if row_mode else 2 * threads))
     batches = [(o, c) for c in range(xs) for o in range(stride)]
     order = [batches[(k * 7919) % len(batches)] for k in range(len(batches))] \
@@ -373,18 +429,11 @@ def main() -> None:
         n_node = (cs.node_visits + cs.shadow_node_visits) / q
         n_tri = (cs.tri_tests + cs.shadow_tri_tests) / q
         b_ray = S_RAY + S_NODE * n_node + S_TRI * n_tri
-        per_launch_rays = (ext_rays + sh_rays) / ext_launches
-        avg_launch_ms = ext_ms / ext_launches
-        achieved = b_ray * per_launch_rays / (avg_launch_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "kernel": ("k_path (persistent: closest-hit + shadow queries + shading)" if args.seed_mode != "row" else
-                           "speculative row engine: k_path<SAMP=2> per iteration; reference-chain rays only "
-                           "(the speculative traces are ~13x as many)"),
-                **pmc_traffic(),
-                "bytes_per_ray": round(b_ray, 1), "n_node_per_ray": round(n_node, 2),
-                "n_tri_per_ray": round(n_tri, 2), "avg_launch_ms": round(avg_launch_ms, 4),
-                "rays_per_launch": round(per_launch_rays, 1)}
+        kernel = ("k_path (persistent: closest-hit + shadow queries + shading)" if args.seed_mode != "row" else
+                  "speculative row engine: k_path<SAMP=2> per iteration; reference-chain rays only "
+                  "(the speculative traces are ~13x as many)")
+        roof = roofline((ext_rays + sh_rays) / ext_launches, ext_ms / ext_launches, b_ray, kernel)
+        roof.update({"n_node_per_query": round(n_node, 2), "n_tri_per_query": round(n_tri, 2)})
 
     # ---- CPU baseline: the reference algorithm on this host, bounded row sample
     cpu = None

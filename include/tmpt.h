@@ -171,7 +171,9 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   rowspec_noshadow speculative row engine: units per window (0 = auto),
  *                    windows per row and iteration (0 = auto, 1..32), window
  *                    spread in pixels (-1 = auto), row groups/streams (1..8),
- *                    shadow-free speculation + one full re-trace (1) */
+ *                    shadow-free speculation + one full re-trace (1)
+ *   wf_bins          wavefront engine: each segment's extend queue split by the
+ *                    rays' direction octant into 1, 2, 4 or 8 sub-queues (1) */
 int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);
 int tmpt_scene_set_option(tmpt_scene* scene, const char* key, double value);
 int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* value);

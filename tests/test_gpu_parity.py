@@ -312,6 +312,25 @@ def test_pixel_mode_matches_oracle(gpu, engine, name, w, h, spp):
     sc.close()
 
 
+@pytest.mark.parametrize("bins", [2, 8])
+def test_wavefront_octant_binned_queues(gpu, bins):
+    """Wavefront engine with each segment's extend queue split by direction
+    octant (option wf_bins, sort-by-bounce binning): the same pixels and ray
+    count as the oracle, on a frame and on a ragged shard."""
+    tris, bmin, bmax, sc = _scene("teapot.obj")
+    sc.set_option("wf_bins", bins)
+    w, h, spp = 320, 180, 4
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT)
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL)
+    assert rays == ref_rays and np.array_equal(img, ref)
+    tile, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT, band_rows=7,
+                             shard=2, num_shards=3)
+    assert np.array_equal(tile, ref[tm.tile_row_to_y(w, h, 7, 2, 3)])
+    sc.close()
+
+
 @pytest.mark.parametrize("engine", [tm.ENGINE_WAVEFRONT, tm.ENGINE_PERSISTENT])
 def test_shards_assemble_to_full_frame(gpu, engine):
     """Interleaved 16-row bands over 3 shards reassemble to the 1-shard frame."""

@@ -123,6 +123,7 @@ const OptionDef kOptions[] = {
     {"rowspec_spread", false, -1, 100, nullptr, &Options::rowspec_spread, nullptr},
     {"rowspec_groups", false, 1, kRowSpecMaxGroups, &Options::rowspec_groups, nullptr, nullptr},
     {"rowspec_noshadow", false, 0, 1, &Options::rowspec_noshadow, nullptr, nullptr},
+    {"wf_bins", false, 1, 8, &Options::wf_bins, nullptr, nullptr},
 };
 
 const OptionDef* find_option(const char* key)
@@ -154,8 +155,9 @@ int options_set(Options& o, const char* key, double v, bool allow_build)
             set_error(std::string("option '") + key + "' takes an integer");
             return -22;
         }
-        if (strcmp(key, "sample_block") == 0 && v > 0 && ((long long)v & ((long long)v - 1)) != 0) {
-            set_error("option 'sample_block' must be a power of two (or 0 = auto)");
+        if ((strcmp(key, "sample_block") == 0 || strcmp(key, "wf_bins") == 0) && v > 0 &&
+            ((long long)v & ((long long)v - 1)) != 0) {
+            set_error(std::string("option '") + key + "' must be a power of two");
             return -22;
         }
         o.*(d->i) = (int)v;

@@ -92,6 +92,7 @@ struct Options {
     float rowspec_spread = -1.0f;  // row seeding: window spread in pixels (-1 = auto)
     int rowspec_groups = 2;   // row seeding: row groups on their own streams
     int rowspec_noshadow = 1; // row seeding: shadow-free speculation + one full re-trace of the chain
+    int wf_bins = 1;          // wavefront engine: extend sub-queues per segment by direction octant (1, 2, 4, 8)
 };
 int options_parse(Options& o, const char* text, bool allow_build);
 int options_set(Options& o, const char* key, double value, bool allow_build);

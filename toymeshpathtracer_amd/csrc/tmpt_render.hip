@@ -279,9 +279,15 @@ struct WfState {
     float* hit;    // [3][P]  t u v
     int32_t* hid;  // [P]
     float* sho;    // [3][P] shadow origin
-    uint32_t* q[2];  // extend queues (per parity), kSeg * seg_cap entries
-    uint32_t* qs;    // shadow queue
-    uint32_t* cnt[2];  // extend queue counts per parity, kSeg counters (stride kCtr)
+    // Extend queues (per parity): kSeg * nbins sub-queues of seg_cap entries,
+    // sub-queue seg * nbins + bin holding the rays of segment seg whose
+    // direction falls in octant bin (the low log2(nbins) bits of the sign
+    // mask; nbins = 1: no binning), so a wave's 64-entry reservation holds
+    // rays from nearby pixels in one octant (sort-by-bounce: every iteration's
+    // queue is one bounce).  Counters and fetch heads per sub-queue.
+    uint32_t* q[2];
+    uint32_t* qs;    // shadow queue: kSeg segments (shadow rays share one direction)
+    uint32_t* cnt[2];  // extend sub-queue counts per parity, kSeg * nbins counters (stride kCtr)
     uint32_t* cnt_s;   // shadow queue counts
     uint32_t* head_e;  // fetch heads
     uint32_t* head_s;
@@ -290,16 +296,24 @@ struct WfState {
     unsigned long long* tot;  // [0] extend rays [1] shadow rays [2,3] extend node/tri visits [4,5] shadow
     int64_t P;
     uint32_t seg_cap;
+    uint32_t nbins;  // 1, 2, 4 or 8
 };
+
+// octant bin of a direction: bit 0 = x < 0, bit 1 = y < 0, bit 2 = z < 0, low bits only
+__device__ __forceinline__ uint32_t dir_bin(f3 d, uint32_t nbins)
+{
+    const uint32_t o = (uint32_t)signbit(d.x) | ((uint32_t)signbit(d.y) << 1) | ((uint32_t)signbit(d.z) << 2);
+    return o & (nbins - 1u);
+}
 
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 {
     int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (p < kSeg) {  // initial queue: every slot, in slot order
+    if (p < kSeg) {  // initial queue: every slot, in slot order, in bin 0 of its segment
         int64_t lo = p * s.seg_cap;
         int64_t c = s.P - lo;
-        s.cnt[0][p * kCtr] = (uint32_t)(c < 0 ? 0 : (c > s.seg_cap ? s.seg_cap : c));
+        s.cnt[0][p * s.nbins * kCtr] = (uint32_t)(c < 0 ? 0 : (c > s.seg_cap ? s.seg_cap : c));
     }
     if (p >= s.P) return;
     int lr = (int)(p / a.W), x = (int)(p - (int64_t)lr * a.W);
@@ -314,7 +328,8 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
     s.col[p] = 0.0f; s.col[P + p] = 0.0f; s.col[2 * P + p] = 0.0f;
     s.ray[p] = o.x; s.ray[P + p] = o.y; s.ray[2 * P + p] = o.z;
     s.ray[3 * P + p] = d.x; s.ray[4 * P + p] = d.y; s.ray[5 * P + p] = d.z;
-    s.q[0][p] = (uint32_t)p;  // segment j starts at j*seg_cap = its first slot
+    const int64_t seg = p / s.seg_cap;  // sub-queue (seg, 0) starts at seg * nbins * seg_cap
+    s.q[0][seg * s.nbins * s.seg_cap + (p - seg * s.seg_cap)] = (uint32_t)p;
 }
 
 // Persistent traversal with lane refill ("dynamic fetch", Aila & Laine 2009,
@@ -343,7 +358,8 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
     const f3 ldir = light_dir();
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     const uint32_t wave_gid = (uint32_t)(gtid >> 6);
-    uint32_t seg = wave_gid % kSeg;  // current segment; starts spread over the frame
+    const uint32_t nq = ANY ? (uint32_t)kSeg : (uint32_t)kSeg * s.nbins;  // sub-queues
+    uint32_t seg = wave_gid % nq;  // current sub-queue; starts spread over the frame
     bool drained = false;
     uint32_t walked = 0;
     uint32_t res = 0, res_end = 0;          // reservation [res, res_end) of queue positions
@@ -358,15 +374,19 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
         if (nidle >= (uint32_t)REFILL && (res < res_end || !drained)) {
             while (res >= res_end && !drained) {  // renew the reservation (wave-uniform)
                 const uint32_t c = counts[seg * kCtr];
-                uint32_t b = 0;
-                if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
-                b = (uint32_t)__shfl((int)b, 0);
+                uint32_t b = c;
+                // a relaxed look at the head first: an empty or consumed
+                // sub-queue costs no atomic (most of the binned ones are)
+                if (c != 0 && __hip_atomic_load(&heads[seg * kCtr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
+                    if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
+                    b = (uint32_t)__shfl((int)b, 0);
+                }
                 if (b < c) {
                     res = seg * s.seg_cap + b;
                     res_end = seg * s.seg_cap + min(b + kChunk, c);
-                } else {  // sequential walk: try the next segment, give up after all 64
-                    seg = (seg + 1) & 63u;
-                    if (++walked == kSeg) drained = true;
+                } else {  // sequential walk: try the next sub-queue, give up after all of them
+                    seg = seg + 1 == nq ? 0u : seg + 1;
+                    if (++walked == nq) drained = true;
                 }
             }
             uint32_t take = min(nidle, res_end - res);
@@ -458,6 +478,7 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
     const uint32_t seg = (uint32_t)(((int64_t)blockIdx.x * BLOCK) / s.seg_cap);
     uint32_t depth = p64 < P ? s.depth[p] : kDone;
     bool cont = false, shadow = false;
+    uint32_t bin = 0;  // octant bin of the next extend ray
     if (depth != kDone) {
         uint32_t rng = s.rng[p];
         f3 d = mk(s.ray[3 * P + p], s.ray[4 * P + p], s.ray[5 * P + p]);
@@ -507,12 +528,18 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
         }
         s.depth[p] = depth;
         s.rng[p] = rng;
+        if (cont && depth != (uint32_t)kMaxDepth) bin = dir_bin(d, s.nbins);
     }
-    const uint32_t base = seg * s.seg_cap;
-    uint32_t qi = wave_append(&s.cnt[parity ^ 1][seg * kCtr], cont);
-    if (cont) s.q[parity ^ 1][base + qi] = depth == (uint32_t)kMaxDepth ? (p | kSkip) : p;
+    // the next extend ray into its (segment, octant) sub-queue: one ballot
+    // and at most one atomic per wave and bin
+    for (uint32_t b = 0; b < s.nbins; ++b) {
+        const bool mine = cont && bin == b;
+        const uint32_t sq = seg * s.nbins + b;
+        const uint32_t qi = wave_append(&s.cnt[parity ^ 1][sq * kCtr], mine);
+        if (mine) s.q[parity ^ 1][sq * s.seg_cap + qi] = depth == (uint32_t)kMaxDepth ? (p | kSkip) : p;
+    }
     uint32_t si = wave_append(&s.cnt_s[seg * kCtr], shadow);
-    if (shadow) s.qs[base + si] = p;
+    if (shadow) s.qs[seg * s.seg_cap + si] = p;
 }
 
 // after the extend of `parity` was consumed: zero its counts and the heads;
@@ -520,18 +547,22 @@ __global__ void __launch_bounds__(BLOCK) k_wf_shade(SceneView sv, RenderArgs a, 
 __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int it)
 {
     int j = threadIdx.x;
-    uint32_t next = s.cnt[parity ^ 1][j * kCtr];
+    uint32_t next = 0, cur = 0;
+    for (uint32_t k = (uint32_t)j; k < (uint32_t)kSeg * s.nbins; k += kSeg) {  // extend sub-queues
+        next += s.cnt[parity ^ 1][k * kCtr];
+        cur += s.cnt[parity][k * kCtr];
+        s.cnt[parity][k * kCtr] = 0;
+        s.head_e[k * kCtr] = 0;
+    }
     if (s.iter_log) {  // debug: rays of this iteration's extend (consumed queue) and shadow
-        uint32_t e = wave_sum(s.cnt[parity][j * kCtr]);
+        uint32_t e = wave_sum(cur);
         uint32_t sh = wave_sum(s.cnt_s[j * kCtr]);
         if (j == 0) {
             s.iter_log[2 * it] = e;
             s.iter_log[2 * it + 1] = sh;
         }
     }
-    s.cnt[parity][j * kCtr] = 0;
     s.cnt_s[j * kCtr] = 0;
-    s.head_e[j * kCtr] = 0;
     s.head_s[j * kCtr] = 0;
     next = wave_sum(next);
     if (j == 0) s.total[0] = next;
@@ -1571,17 +1602,18 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     int grid_t = occupancy_grid((const void*)trace_e, kBlk, 0, s.device);
     const int grid_sh = (int)((P + kBlk - 1) / kBlk);
     const size_t seg_cap = (size_t)(((P + kSeg - 1) / kSeg + kBlk - 1) / kBlk) * kBlk;
-    const size_t qcap = seg_cap * kSeg;
+    const uint32_t nbins = (uint32_t)s.opt.wf_bins;  // extend sub-queues per segment (octant bins)
+    const size_t qcap = seg_cap * kSeg * nbins, qcap_s = seg_cap * kSeg;
     const size_t Pz = (size_t)P;
     size_t ovf_words = (size_t)grid_t * kBlk * (kStackTotal - sl);
     // layout of the workspace
     size_t words = 0;
     auto take = [&](size_t w) { size_t o = words; words += (w + 63) & ~size_t(63); return o; };
-    const size_t ctr_words = (size_t)kSeg * kCtr;
+    const size_t ctr_words = (size_t)kSeg * kCtr, ectr_words = ctr_words * nbins;
     size_t o_rng = take(Pz), o_smp = take(Pz), o_depth = take(Pz), o_col = take(3 * Pz),
            o_light = take(kMaxDepth * Pz), o_ray = take(6 * Pz), o_hit = take(3 * Pz),
            o_hid = take(Pz), o_sho = take(3 * Pz), o_q0 = take(qcap), o_q1 = take(qcap),
-           o_qs = take(qcap), o_ctl = take(5 * ctr_words + 64), o_tot = take(16),
+           o_qs = take(qcap_s), o_ctl = take(3 * ectr_words + 2 * ctr_words + 64), o_tot = take(16),
            o_ovf = take(ovf_words);
 #ifdef TMPT_DIAG
     const bool log_iters = getenv("TMPT_ITER_LOG") != nullptr;  // diagnostic build: queue sizes per iteration
@@ -1606,19 +1638,20 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     st.q[1] = w + o_q1;
     st.qs = w + o_qs;
     st.cnt[0] = w + o_ctl;
-    st.cnt[1] = st.cnt[0] + ctr_words;
-    st.cnt_s = st.cnt[1] + ctr_words;
-    st.head_e = st.cnt_s + ctr_words;
-    st.head_s = st.head_e + ctr_words;
+    st.cnt[1] = st.cnt[0] + ectr_words;
+    st.head_e = st.cnt[1] + ectr_words;
+    st.cnt_s = st.head_e + ectr_words;
+    st.head_s = st.cnt_s + ctr_words;
     st.total = st.head_s + ctr_words;
     st.tot = (unsigned long long*)(w + o_tot);
     st.iter_log = log_iters ? w + o_log : nullptr;
     st.P = P;
     st.seg_cap = (uint32_t)seg_cap;
+    st.nbins = nbins;
     uint32_t* ovf = w + o_ovf;
     hipStream_t str = s.stream;
 
-    TMPT_HIP(hipMemsetAsync(w + o_ctl, 0, (5 * ctr_words + 64) * 4, str));
+    TMPT_HIP(hipMemsetAsync(w + o_ctl, 0, (3 * ectr_words + 2 * ctr_words + 64) * 4, str));
     TMPT_HIP(hipMemsetAsync(st.tot, 0, 8 * sizeof(unsigned long long), str));
     if (st.iter_log) TMPT_HIP(hipMemsetAsync(st.iter_log, 0, 8 * (size_t)max_log, str));
     k_wf_generate<kBlk><<<(int)((std::max<int64_t>(P, kSeg) + kBlk - 1) / kBlk), kBlk, 0, str>>>(a, st);
