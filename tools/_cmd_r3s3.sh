@@ -4,8 +4,6 @@
 out=gpurun_out/r03s3; mkdir -p $out; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "octant or pixel_mode or render_multi or ranges" > $out/pytest_sel.log 2>&1
 rc=$?; tail -2 $out/pytest_sel.log; if [ $rc -ne 0 ]; then grep -E "FAIL|Error" $out/pytest_sel.log | head; exit $rc; fi
-timeout -k 10 300 python -u tools/tune.py "ENGINE=wavefront;ENGINE=wavefront&wf_bins=2;ENGINE=wavefront&wf_bins=8;ENGINE=persistent" 64 3 > $out/tune_bins.log 2>&1 || exit $?
-cat $out/tune_bins.log | tail -5
 for v in "ENGINE=wavefront" "ENGINE=wavefront&wf_bins=8"; do
   tag=wf_$(echo $v | tr '=&' '__')
   timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE -d $out/$tag -o run -- python3 tools/tune.py "$v" 64 1 > $out/$tag.log 2>&1
@@ -23,4 +21,9 @@ for set in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-compare > $out/prof_bench.json 2> $out/prof.err
 echo "prof rc=$?"
+# summaries on the box (the rocpd databases exceed the 64 MiB pull limit)
+python3 tools/roofline_counters.py $out/pmc $out/pmc > $out/counters_k_path.json 2> $out/counters.err
+python3 tools/prof_summary.py $out/prof/run_results.db > $out/rocprof_stats.txt 2>&1
+python3 tools/wf_counters.py $out > $out/wf_counters.txt 2>&1
+find $out -name "*.db" -delete
 echo session-done
