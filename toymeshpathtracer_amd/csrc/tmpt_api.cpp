@@ -393,6 +393,10 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.rs_host) (void)hipHostFree(s.rs_host);
     if (s.rs_list) (void)hipFree(s.rs_list);
     if (s.wait_ev) (void)hipEventDestroy(s.wait_ev);
+    if (s.counters) (void)hipFree(s.counters);
+    if (s.counters_host) (void)hipHostFree(s.counters_host);
+    for (auto e : s.render_ev)
+        if (e) (void)hipEventDestroy(e);
     if (s.tri_pre) (void)hipFree(s.tri_pre);
     if (s.tri_orig) (void)hipFree(s.tri_orig);
     if (s.ws) (void)hipFree(s.ws);

@@ -66,6 +66,7 @@ constexpr float kTfarSlack = 1.00001f;
 constexpr int kStackTotal = 128;
 
 constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
+constexpr int kRenderCounters = 24;   // ray / visit / round counters of one render
 
 // Per-scene options: the library's control plane in place of environment
 // variables (include/tmpt.h documents each key).  Build options are fixed when
@@ -109,6 +110,9 @@ struct Scene {
     TriOrig* tri_orig = nullptr;
     Options opt;  // build and render options (tmpt_scene_create_ex / tmpt_scene_set_option)
     hipEvent_t wait_ev = nullptr;  // TMPT_FLAG_WAIT_STREAM: reused across renders
+    unsigned long long* counters = nullptr;       // a render's ray / visit counters (device)
+    unsigned long long* counters_host = nullptr;  // their pinned host copy
+    hipEvent_t render_ev[2] = {nullptr, nullptr}; // first / last kernel of a render
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
     // render workspace (grown on demand, reused across calls)

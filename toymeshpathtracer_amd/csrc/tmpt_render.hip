@@ -2348,13 +2348,18 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
             return -1;
         }
     }
-    unsigned long long* d_counters = nullptr;
-    constexpr int kCounters = 24;
-    TMPT_HIP(hipMallocAsync((void**)&d_counters, kCounters * sizeof(unsigned long long), s.stream));
-    TMPT_HIP(hipMemsetAsync(d_counters, 0, kCounters * sizeof(unsigned long long), s.stream));
-    hipEvent_t e0, e1;
-    TMPT_HIP(hipEventCreate(&e0));
-    TMPT_HIP(hipEventCreate(&e1));
+    // the render's counters (device) and their pinned host copy, and the two
+    // timing events: created once per scene, so a render call costs no
+    // allocation (it matters for the small shards of a multi-GPU frame)
+    if (!s.counters) {
+        TMPT_HIP(hipMalloc(&s.counters, kRenderCounters * sizeof(unsigned long long)));
+        TMPT_HIP(hipHostMalloc((void**)&s.counters_host, kRenderCounters * sizeof(unsigned long long),
+                               hipHostMallocDefault));
+        for (auto& e : s.render_ev) TMPT_HIP(hipEventCreate(&e));
+    }
+    unsigned long long* d_counters = s.counters;
+    TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
+    hipEvent_t e0 = s.render_ev[0], e1 = s.render_ev[1];
     TMPT_HIP(hipEventRecord(e0, s.stream));
     int rc = 0;
     const bool wave = d->engine == TMPT_ENGINE_WAVEFRONT && a.seed_mode != TMPT_SEED_ROW;
@@ -2366,9 +2371,6 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
                          !progressive && s.opt.rowspec != 0;
     if (progressive && !persistent) {
         set_error("tmpt_render: progressive spp needs the persistent engine");
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        (void)hipFreeAsync(d_counters, s.stream);
         return -22;
     }
     s.extend_ms = s.shadow_ms = 0;
@@ -2382,15 +2384,15 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         else rc = render_megakernel(s, a, d_out, count, d_counters);
     }
     (void)hipEventRecord(e1, s.stream);
-    hipError_t se = hipStreamSynchronize(s.stream);
-    unsigned long long c[kCounters] = {};
-    if (rc == 0 && se == hipSuccess)
-        se = hipMemcpy(c, d_counters, sizeof(c), hipMemcpyDeviceToHost);
+    hipError_t se = rc == 0 ? hipMemcpyAsync(s.counters_host, d_counters, kRenderCounters * sizeof(unsigned long long),
+                                             hipMemcpyDeviceToHost, s.stream)
+                            : hipSuccess;
+    const hipError_t se2 = hipStreamSynchronize(s.stream);
+    if (se == hipSuccess) se = se2;
+    unsigned long long c[kRenderCounters] = {};
+    if (rc == 0 && se == hipSuccess) memcpy(c, s.counters_host, sizeof(c));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipFreeAsync(d_counters, s.stream);
     if (rc) return rc;
     if (se != hipSuccess) {
         set_error(std::string("render: ") + hipGetErrorString(se));
