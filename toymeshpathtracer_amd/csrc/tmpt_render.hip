@@ -263,6 +263,9 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
 // instead of serialising on one (MI355X_MICROARCH.md: one word saturates at
 // ~88 atomics/us).
 constexpr int kSeg = 64;  // == wave width: one lane probes one segment
+#ifndef TMPT_WF_TOPC  // wavefront traversal reads the top BVH4 levels from an LDS copy
+#define TMPT_WF_TOPC 1
+#endif
 static_assert(kSeg == 64, "segment probing maps segments to the 64 lanes of a wave");
 constexpr int kCtr = 16;  // words between counters (64 B)
 constexpr uint32_t kChunk = 64;  // queue entries a wave reserves per atomic
@@ -349,6 +352,15 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
     __shared__ uint32_t s_stack[SL * BLOCK];
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    if (TMPT_WF_TOPC) {  // the top BVH4 levels in LDS (as k_path)
+        __shared__ uint4 s_top[TMPT_WF_TOPC ? kTopNodes * 4 : 1];
+        const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
+        const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
+        for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
+        __syncthreads();
+        st.top = (const lds_u4*)s_top;
+        st.ntop = ntop;
+    }
     TravCount cnt;
     uint32_t traced = 0;
     const uint32_t* q = ANY ? s.qs : s.q[parity];
@@ -429,8 +441,15 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
                 const uint64_t at_node = wballot(!done && ts.node >= 0);
                 if (at_leaf == 0 && at_node == 0) break;
                 const bool leaf_round = __popcll(at_leaf) > __popcll(at_node);
-                if (!done && (ts.node < 0) == leaf_round) {
-                    done = trav_step4q2_mixed<COUNT, BLOCK, SL>(sv, r, ANY, ts, st, cnt);
+                // the kind is wave-uniform: a scalar branch to the step that has
+                // only that kind's code (as in k_path's voted rounds)
+                if (leaf_round) {
+                    if (!done && ts.node < 0) {
+                        done = trav_step4q2_mixed<COUNT, BLOCK, SL, TMPT_WF_TOPC, 2>(sv, r, ANY, ts, st, cnt);
+                        if (COUNT) ++steps;
+                    }
+                } else if (!done && ts.node >= 0) {
+                    done = trav_step4q2_mixed<COUNT, BLOCK, SL, TMPT_WF_TOPC, 1>(sv, r, ANY, ts, st, cnt);
                     if (COUNT) ++steps;
                 }
             }
