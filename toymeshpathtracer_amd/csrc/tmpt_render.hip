@@ -263,9 +263,6 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
 // instead of serialising on one (MI355X_MICROARCH.md: one word saturates at
 // ~88 atomics/us).
 constexpr int kSeg = 64;  // == wave width: one lane probes one segment
-#ifndef TMPT_WF_TOPC  // wavefront traversal reads the top BVH4 levels from an LDS copy
-#define TMPT_WF_TOPC 1
-#endif
 static_assert(kSeg == 64, "segment probing maps segments to the 64 lanes of a wave");
 constexpr int kCtr = 16;  // words between counters (64 B)
 constexpr uint32_t kChunk = 64;  // queue entries a wave reserves per atomic
@@ -300,6 +297,7 @@ struct WfState {
     int64_t P;
     uint32_t seg_cap;
     uint32_t nbins;  // 1, 2, 4 or 8
+    int walk_check;  // relaxed head check before a walking wave's atomic (low load, binned queues)
 };
 
 // octant bin of a direction: bit 0 = x < 0, bit 1 = y < 0, bit 2 = z < 0, low bits only
@@ -345,15 +343,15 @@ __global__ void __launch_bounds__(BLOCK) k_wf_generate(RenderArgs a, WfState s)
 // waves work on nearby pixels and the heads see few atomics.  Lanes run
 // STEPS traversal steps between refill checks, each step of the kind (node or
 // leaf) more lanes are waiting for.
-template <bool ANY, bool COUNT, int BLOCK, int SL, int STEPS = 4, int REFILL = 8>
-__global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int parity,
-                                                    uint32_t* __restrict__ ovf)
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC, int MINW, int STEPS = 4, int REFILL = 8>
+__global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState s, int parity,
+                                                          uint32_t* __restrict__ ovf)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
-    if (TMPT_WF_TOPC) {  // the top BVH4 levels in LDS (as k_path)
-        __shared__ uint4 s_top[TMPT_WF_TOPC ? kTopNodes * 4 : 1];
+    if (TOPC) {  // the top BVH4 levels in LDS (as k_path)
+        __shared__ uint4 s_top[TOPC ? kTopNodes * 4 : 1];
         const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
         const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
         for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
@@ -387,15 +385,21 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
             while (res >= res_end && !drained) {  // renew the reservation (wave-uniform)
                 const uint32_t c = counts[seg * kCtr];
                 uint32_t b = c;
-                // a relaxed look at the head first: an empty or consumed
-                // sub-queue costs no atomic (most of the binned ones are)
-                if (c != 0 && __hip_atomic_load(&heads[seg * kCtr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
+                // at low load (walk_check) a wave walking past its own
+                // sub-queue takes a relaxed look at the head first, so an
+                // exhausted sub-queue costs no atomic (every wave walks all of
+                // them at the end of an iteration: 1/8 shard 310 -> 193 ms);
+                // at full load that extra round trip per renewal costs more
+                // than it saves (N = 1: 550 -> 773 ms), so the atomic alone
+                if (c != 0 && (walked == 0 || !s.walk_check ||
+                               __hip_atomic_load(&heads[seg * kCtr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c)) {
                     if (lane_id() == 0) b = atomicAdd(&heads[seg * kCtr], kChunk);
                     b = (uint32_t)__shfl((int)b, 0);
                 }
                 if (b < c) {
                     res = seg * s.seg_cap + b;
                     res_end = seg * s.seg_cap + min(b + kChunk, c);
+                    walked = 0;
                 } else {  // sequential walk: try the next sub-queue, give up after all of them
                     seg = seg + 1 == nq ? 0u : seg + 1;
                     if (++walked == nq) drained = true;
@@ -445,11 +449,11 @@ __global__ void __launch_bounds__(BLOCK) k_wf_trace(SceneView sv, WfState s, int
                 // only that kind's code (as in k_path's voted rounds)
                 if (leaf_round) {
                     if (!done && ts.node < 0) {
-                        done = trav_step4q2_mixed<COUNT, BLOCK, SL, TMPT_WF_TOPC, 2>(sv, r, ANY, ts, st, cnt);
+                        done = trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 2>(sv, r, ANY, ts, st, cnt);
                         if (COUNT) ++steps;
                     }
                 } else if (!done && ts.node >= 0) {
-                    done = trav_step4q2_mixed<COUNT, BLOCK, SL, TMPT_WF_TOPC, 1>(sv, r, ANY, ts, st, cnt);
+                    done = trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 1>(sv, r, ANY, ts, st, cnt);
                     if (COUNT) ++steps;
                 }
             }
@@ -1615,8 +1619,12 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
         set_error("wavefront: tile too large");
         return -22;
     }
-    auto trace_e = count ? k_wf_trace<false, true, kBlk, kSL> : k_wf_trace<false, false, kBlk, kSL>;
-    auto trace_s = count ? k_wf_trace<true, true, kBlk, kSL> : k_wf_trace<true, false, kBlk, kSL>;
+    // top BVH levels from LDS in both passes, no occupancy floor: measured best
+    // against no LDS copy and 5-8 waves per SIMD (profiles/r03_wavefront_ab/)
+    constexpr bool kTopE = true, kTopS = true;
+    constexpr int kWE = 1, kWS = 1;
+    auto trace_e = count ? k_wf_trace<false, true, kBlk, kSL, kTopE, kWE> : k_wf_trace<false, false, kBlk, kSL, kTopE, kWE>;
+    auto trace_s = count ? k_wf_trace<true, true, kBlk, kSL, kTopS, kWS> : k_wf_trace<true, false, kBlk, kSL, kTopS, kWS>;
     const int sl = kSL;
     int grid_t = occupancy_grid((const void*)trace_e, kBlk, 0, s.device);
     const int grid_sh = (int)((P + kBlk - 1) / kBlk);
@@ -1667,6 +1675,9 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     st.P = P;
     st.seg_cap = (uint32_t)seg_cap;
     st.nbins = nbins;
+    // low load: under two queue entries per resident traversal lane; binned
+    // queues always (most of their sub-queues are empty)
+    st.walk_check = nbins > 1 || P < 2 * (int64_t)grid_t * kBlk;
     uint32_t* ovf = w + o_ovf;
     hipStream_t str = s.stream;
 
