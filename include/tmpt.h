@@ -168,10 +168,14 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   rowspec          row seeding on the persistent engine: 1 = speculative row
  *                    engine, 0 = one lane per row chain
  *   rowspec_wmax, rowspec_windows, rowspec_spread, rowspec_groups,
- *   rowspec_noshadow speculative row engine: units per window (0 = auto),
+ *   rowspec_noshadow, rowspec_chase, rowspec_stream
+ *                    speculative row engine: units per window (0 = auto),
  *                    windows per row and iteration (0 = auto, 1..32), window
  *                    spread in pixels (-1 = auto), row groups/streams (1..8),
- *                    shadow-free speculation + one full re-trace (1)
+ *                    shadow-free speculation + one full re-trace (1), the
+ *                    chase over LDS-staged units, one wave per row (1), the
+ *                    streaming engine: one launch, chains walked on the device
+ *                    as units finish (1; 0 = host-driven iterations, the default)
  *   wf_bins          wavefront engine: each segment's extend queue split by the
  *                    rays' direction octant into 1, 2, 4 or 8 sub-queues (1) */
 int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);

@@ -212,27 +212,40 @@ def test_row_mode_reproduces_reference_binary(gpu, name, engine):
 
 
 # ---------------------------------------------------------------- speculative row chains
-@pytest.mark.parametrize("opts", [{}, {"rowspec_wmax": 8}, {"rowspec_wmax": 33},
-                                  {"rowspec_windows": 1}, {"rowspec_windows": 1, "rowspec_wmax": 33},
-                                  {"rowspec_spread": 0.0}, {"rowspec_spread": 0.0, "rowspec_wmax": 8},
-                                  {"rowspec_spread": 0.02, "rowspec_windows": 8},
-                                  {"rowspec_windows": 32, "rowspec_groups": 3},
-                                  {"rowspec_noshadow": 0}, {"rowspec_noshadow": 0, "rowspec_wmax": 8}])
+_ITER = {"rowspec_stream": 0}    # the host-driven iterations
+_STREAM = {"rowspec_stream": 1}  # the streaming engine
+
+
+@pytest.mark.parametrize("opts", [{}, {**_STREAM}, {**_STREAM, "rowspec_windows": 1}, {**_STREAM, "rowspec_spread": 0.0},
+                                  {**_STREAM, "rowspec_spread": 0.0, "rowspec_windows": 1},
+                                  {**_STREAM, "rowspec_windows": 7},
+                                  {**_ITER}, {**_ITER, "rowspec_wmax": 8}, {**_ITER, "rowspec_wmax": 33},
+                                  {**_ITER, "rowspec_windows": 1}, {**_ITER, "rowspec_windows": 1, "rowspec_wmax": 33},
+                                  {**_ITER, "rowspec_spread": 0.0}, {**_ITER, "rowspec_spread": 0.0, "rowspec_wmax": 8},
+                                  {**_ITER, "rowspec_spread": 0.02, "rowspec_windows": 8},
+                                  {**_ITER, "rowspec_windows": 32, "rowspec_groups": 3},
+                                  {"rowspec_noshadow": 0}, {"rowspec_noshadow": 0, "rowspec_wmax": 8},
+                                  {**_ITER, "rowspec_chase": 0}, {**_ITER, "rowspec_chase": 0, "rowspec_wmax": 33}])
 @pytest.mark.parametrize("name,w,h,spp", [("suzanne.obj", 320, 180, 16), ("teapot.obj", 203, 77, 7),
                                           ("cube.obj", 64, 1, 1), ("triangle.obj", 1, 3, 5)])
 def test_rowspec_equals_row_chains(gpu, name, w, h, spp, opts):
-    """The speculative row engine (every even RNG offset of a window traced,
+    """The speculative row engines (every even RNG offset of a window traced,
     then the chain walked through it, into the next pixel's lookahead window
-    when its first sample falls there) gives the one-lane-per-row megakernel's
-    image and ray count exactly: windows capped at 8 and 33 units, or placed
-    with no spread, force many iterations per pixel, chains that leave a
-    window mid-pixel and next pixels that start before or after the lookahead."""
+    when its first sample falls there) give the one-lane-per-row megakernel's
+    image and ray count exactly.  Iterated engine: windows capped at 8 and 33
+    units, or placed with no spread, force many iterations per pixel, chains
+    that leave a window mid-pixel and next pixels that start before or after
+    the lookahead.  Streaming engine: one window ahead or seven, no spread
+    (most pixels then need the chaser's demand or extension windows)."""
     tris, bmin, bmax, sc = _scene(name)
     for k, v in opts.items():
         sc.set_option(k, v)
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
     b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    if opts.get("rowspec_stream") == 1:
+        # the streaming engine ran (one launch), not its fallback to iterations
+        assert sc.stats().iterations == 1
     assert ra == rb
     diff = np.nonzero((a != b).any(-1))
     assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"

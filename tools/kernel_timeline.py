@@ -41,6 +41,22 @@ def main():
     print(f"{'kernel':<72} {'n':>5} {'dur_us':>12} {'gap_before_us':>14}")
     for k, (n, d, g) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
         print(f"{k:<72} {n:>5} {d:>12.1f} {g:>14.1f}")
+    # device busy time: the union of all dispatch intervals (kernels on several
+    # streams overlap), against the span from the first start to the last end
+    iv = sorted((s, e) for _, s, e in rows)
+    busy, cs, ce = 0, None, None
+    for s, e in iv:
+        if ce is None or s > ce:
+            if ce is not None:
+                busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    if ce is not None:
+        busy += ce - cs
+        span = max(e for _, e in iv) - iv[0][0]
+        print(f"\nspan {span / 1e6:.3f} ms, device busy (union) {busy / 1e6:.3f} ms ({100.0 * busy / span:.1f} %), "
+              f"sum of durations {sum(e - s for s, e in iv) / 1e6:.3f} ms")
     print(f"\nlast {last} dispatches (duration us, idle gap before it us):")
     for k, d, g in out[-last:]:
         print(f"{k:<72} {d:>10.1f} {g:>10.1f}")

@@ -32,7 +32,8 @@ def main():
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
     sc = tm.Scene(tris)
     defaults = {k: sc.get_option(k) for k in ("rowspec", "rowspec_wmax", "rowspec_windows", "rowspec_spread",
-                                              "rowspec_groups", "rowspec_noshadow")}
+                                              "rowspec_groups", "rowspec_noshadow", "rowspec_chase",
+                                              "rowspec_stream")}
     ref = None
     res = {v: [] for v in variants}
     for _ in range(rounds):

@@ -50,7 +50,8 @@ scenes = {}
 with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after each variant
     DEFAULTS = {k: _probe.get_option(k) for k in ("sample_block", "sbuf_max", "pilot", "help", "pair", "balance", "dprio",
                                                   "wave_cap", "rowspec", "rowspec_wmax", "rowspec_windows",
-                                                  "rowspec_spread", "rowspec_groups", "rowspec_noshadow", "wf_bins")}
+                                                  "rowspec_spread", "rowspec_groups", "rowspec_noshadow", "rowspec_chase", "rowspec_stream",
+                                                  "wf_bins")}
 
 
 def scene_for(env):

@@ -123,6 +123,8 @@ const OptionDef kOptions[] = {
     {"rowspec_spread", false, -1, 100, nullptr, &Options::rowspec_spread, nullptr},
     {"rowspec_groups", false, 1, kRowSpecMaxGroups, &Options::rowspec_groups, nullptr, nullptr},
     {"rowspec_noshadow", false, 0, 1, &Options::rowspec_noshadow, nullptr, nullptr},
+    {"rowspec_chase", false, 0, 1, &Options::rowspec_chase, nullptr, nullptr},
+    {"rowspec_stream", false, 0, 1, &Options::rowspec_stream, nullptr, nullptr},
     {"wf_bins", false, 1, 8, &Options::wf_bins, nullptr, nullptr},
 };
 
@@ -392,6 +394,9 @@ int tmpt_scene_destroy(tmpt_scene* h)
         if (ev) (void)hipEventDestroy(ev);
     if (s.rs_host) (void)hipHostFree(s.rs_host);
     if (s.rs_list) (void)hipFree(s.rs_list);
+    if (s.rss_buf) (void)hipFree(s.rss_buf);
+    if (s.rss_tab) (void)hipFree(s.rss_tab);
+    if (s.rss_host) (void)hipHostFree(s.rss_host);
     if (s.wait_ev) (void)hipEventDestroy(s.wait_ev);
     if (s.counters) (void)hipFree(s.counters);
     if (s.counters_host) (void)hipHostFree(s.counters_host);

@@ -93,6 +93,8 @@ struct Options {
     float rowspec_spread = -1.0f;  // row seeding: window spread in pixels (-1 = auto)
     int rowspec_groups = 2;   // row seeding: row groups on their own streams
     int rowspec_noshadow = 1; // row seeding: shadow-free speculation + one full re-trace of the chain
+    int rowspec_chase = 1;    // row seeding, shadow-free: the chase walks LDS-staged units, one wave per row
+    int rowspec_stream = 0;   // row seeding: the streaming row engine (one launch; 0 = iterations)
     int wf_bins = 1;          // wavefront engine: extend sub-queues per segment by direction octant (1, 2, 4, 8)
 };
 int options_parse(Options& o, const char* text, bool allow_build);
@@ -141,6 +143,12 @@ struct Scene {
     uint32_t* rs_host = nullptr;                        // pinned: each group's last unit count
     void* rs_list = nullptr;                            // no-shadow speculation: the chain list
     size_t rs_list_bytes = 0;
+    // streaming row engine (render_rowstream): rings, windows, anchors; its
+    // jump tables (M^(2c), M^(256b), M^(2^15 a0), M^(2^20 a1)); pinned control words
+    void* rss_buf = nullptr;
+    size_t rss_bytes = 0;
+    uint32_t* rss_tab = nullptr;
+    uint32_t* rss_host = nullptr;
     int path_launches = 1;  // k_path launches of the last persistent render (pilot ordering: 2)
     hipEvent_t path_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // around the pilot / final k_path
     // statistics of the last render

@@ -610,6 +610,49 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 // chunks taken, so all segments together hand out ranks in increasing order
 // (the waves walk segments from their own one, one atomic per chunk).  Rank r
 // is pixel order[r] (a cost-descending order from a pilot pass) or r itself.
+// Streaming row engine (SAMP 4, render_rowstream): the speculative row chains
+// of render_rowspec without iterations.  One persistent launch: chaser waves
+// (the first blocks, one lane per row) walk each row's chain as soon as the
+// unit it needs is done and plan pixel windows ahead of it; worker waves take
+// units from the rows' windows and trace them shadow-free.  A unit (row,
+// pixel p, offset j) starts at M^(2j) row_seed, like render_rowspec's.
+//   slots[row][kRssT + 1]: pixel windows, word = (p+1) << 48 | q << 24 | hi
+//     (offsets [q, hi) of pixel p not handed out yet; slot p % kRssT; the last
+//     slot is the chain's demand window for the current pixel); workers take
+//     offsets by CAS, the chaser plans and extends by CAS
+//   res[row][p % kRssT][j % R]: a finished unit, word = ((p+1) << 24 | j) << 28
+//     | draws | rays << 14 | closest-hit rays << 19, written by atomicMax, so a
+//     late unit of a pixel kRssT back never overwrites a live one
+//   chainpos[row] = x << 32 | c: the chain's pixel and next sample's offset
+//   list[(row * W + x) * spp + k] = offset of sample k of pixel x on the chain
+//   ctl: [0] rows done, [1] abort, [2] chain progress ticks, [3] error, [4] P
+constexpr int kRssT = 8;
+constexpr uint32_t kRssM24 = 0xFFFFFFu;
+struct RsStream {
+    unsigned long long* __restrict__ slots;
+    unsigned long long* __restrict__ res;
+    unsigned long long* __restrict__ chainpos;
+    uint32_t* __restrict__ list;
+    uint32_t* __restrict__ rowrays;    // [row][2]: chain rays, closest-hit
+    uint32_t* __restrict__ lo;         // [row][kRssT]: chaser-private window starts
+    uint32_t* __restrict__ ctl;
+    const uint32_t* __restrict__ anchors;  // [row][na]: M^(2^15 a) row_seed
+    const uint32_t* __restrict__ t1;       // M^(2c), c < 128 (byte tables)
+    const uint32_t* __restrict__ t2;       // M^(256 b), b < 128
+    uint32_t na, R, rmask;
+    uint32_t jlimit;        // na * 2^14: offsets with an anchor
+    int nrows, nchase, nw;  // rows, chaser blocks, live pixel windows per row
+    float spread;
+};
+
+// M^(2j) row_seed of row `row` (j < na * 2^14)
+__device__ __forceinline__ uint32_t rss_state(const RsStream& S, int row, uint32_t j)
+{
+    uint32_t s = S.anchors[(size_t)row * S.na + (j >> 14)];
+    s = sample_seed(S.t2, (j >> 7) & 127u, s);
+    return sample_seed(S.t1, j & 127u, s);
+}
+
 struct PathCtl {
     uint32_t* heads;  // kSeg chunk counters, stride kCtr
     uint32_t nchunks;
@@ -659,6 +702,7 @@ struct PathCtl {
     // sample uslot[u] of its pixel, colour into sbuf (resolved in order)
     int rs_noshadow;
     const uint32_t* __restrict__ uslot;
+    RsStream rss;  // SAMP 4
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -691,6 +735,142 @@ __device__ __forceinline__ uint2 simd_rank(uint32_t* reg)
     return make_uint2((uint32_t)__shfl((int)r, 0), (uint32_t)__shfl((int)d, 0));
 }
 
+__device__ __forceinline__ unsigned long long rss_ld(const unsigned long long* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t rss_ld32(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long rss_win(uint32_t p, uint32_t q, uint32_t hi)
+{
+    return ((unsigned long long)(p + 1u) << 48) | ((unsigned long long)q << 24) | hi;
+}
+
+// The chaser of render_rowstream: lane = row.  Walks the row's chain through
+// the finished units (k_rs_chase's walk, main.cpp:209-219), records each chain
+// sample's offset, plans pixel windows ahead (k_rs_plan's placement: pixel x + i
+// expected i - 1 pixels after the current pixel's expected end, +- spread *
+// sqrt(i) pixels) and, when the chain needs an offset no window covers, opens
+// it (the demand window for a start before the current window, an extension
+// past its end).  Exits when its rows are done or the launch aborts.
+template <int BLOCK>
+__device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
+{
+    const int row = wave * 64 + lane_id();
+    const bool mine = row < S.nrows;
+    const uint32_t W = (uint32_t)a.W, spp = (uint32_t)a.spp, T = (uint32_t)kRssT;
+    uint32_t c = 0, x = 0, k = 0, pdraws = 0, rays = 0, erays = 0, planned = 0;
+    uint32_t n_wait = 0, n_ext = 0, n_pre = 0, n_sweep = 0;  // statistics (ctl[8..11])
+    uint32_t stuck = 0;  // sweeps the chain has waited at the same (x, c)
+    float mean = 17.0f;  // draws per sample before any is seen (k_rs_init)
+    bool done = !mine, err = false;
+    unsigned long long* slot = S.slots + (size_t)(mine ? row : 0) * (T + 1u);
+    uint32_t* lo = S.lo + (size_t)(mine ? row : 0) * T;
+    const unsigned long long* res = S.res + (size_t)(mine ? row : 0) * T * S.R;
+    const uint32_t cap_span = S.R - 64u;  // live offsets ahead of the chain: under one ring
+    // plan pixel q (> x) from the chain's position
+    auto plan = [&](uint32_t q) {
+        const float E = (float)spp * mean * 0.5f, rest = (float)(spp - k) * mean * 0.5f;
+        const float i = (float)(q - x);
+        const float P = (float)c + rest + (i - 1.0f) * E;
+        const float lo_f = fmaxf((float)c, P - S.spread * sqrtf(i) * E);
+        const float hi_f = P + E + S.spread * sqrtf(i + 1.0f) * E + 2.0f;
+        const uint32_t l = (uint32_t)lo_f, h = min((uint32_t)hi_f, c + cap_span);
+        lo[q % T] = l;
+        __hip_atomic_exchange(&slot[q % T], rss_win(q, min(l, h), h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (mine) {  // the first pixel from offset 0, then the lookahead windows
+        const float E = (float)spp * mean * 0.5f;
+        const uint32_t h = min((uint32_t)(E + S.spread * E) + 2u, cap_span);
+        lo[0] = 0;
+        __hip_atomic_exchange(&slot[0], rss_win(0, 0, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        planned = 0;
+        while (planned + 1u < min(W, (uint32_t)S.nw)) plan(++planned);
+    }
+    for (;;) {
+        bool moved = false;
+        if (!done) {
+            for (int it = 0; it < 64; ++it) {
+                const unsigned long long w = rss_ld(res + (size_t)(x % T) * S.R + (c & S.rmask));
+                if ((w >> 28) != (((unsigned long long)(x + 1u) << 24) | c)) {
+                    // not finished, or no window holds (x, c): looked at once
+                    // the chain has waited two sweeps (usually the unit is in flight)
+                    if (++stuck < 3u) break;
+                    stuck = 0;
+                    const unsigned long long sw = rss_ld(&slot[x % T]);
+                    const uint32_t q = (uint32_t)(sw >> 24) & kRssM24, hi = (uint32_t)sw & kRssM24;
+                    const uint32_t l = lo[x % T];
+                    const uint32_t rest = (uint32_t)((float)(spp - k) * mean * 0.65f) + 16u;
+                    ++n_wait;
+                    if (c < l) {  // the pixel starts before its window: demand [c, l)
+                        ++n_pre;
+                        __hip_atomic_exchange(&slot[T], rss_win(x, c, min(l, c + cap_span)), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                        lo[x % T] = c;
+                    } else if (c >= hi) {  // past the window's end: a new window from c
+                        // (everything below hi was handed out; the workers' adds
+                        // past hi handed out nothing, so q restarts at c)
+                        ++n_ext;
+                        __hip_atomic_exchange(&slot[x % T], rss_win(x, c, c + min(rest, cap_span)),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    (void)q;
+                    break;
+                }
+                stuck = 0;
+                const uint32_t draws = (uint32_t)w & 0x3FFFu;
+                rays += (uint32_t)(w >> 14) & 31u;
+                erays += (uint32_t)(w >> 19) & 15u;
+                pdraws += draws;
+                S.list[((size_t)row * W + x) * spp + k] = c;  // sample k of pixel x: offset c
+                c += draws >> 1;
+                moved = true;
+                if (c + cap_span >= S.jlimit) {  // offsets past the anchors (or 24-bit words): abort, fall back
+                    err = true;
+                    done = true;
+                    break;
+                }
+                if (++k == spp) {  // pixel done (main.cpp:221-233 packs it in the final pass)
+                    mean = (float)pdraws / (float)k;
+                    k = 0;
+                    pdraws = 0;
+                    if (++x == W) {
+                        done = true;
+                        break;
+                    }
+                    while (planned + 1u < W && planned < x + (uint32_t)S.nw - 1u) plan(++planned);
+                }
+            }
+            if (moved) __hip_atomic_store(&S.chainpos[row], ((unsigned long long)x << 32) | c, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            if (done) {
+                S.rowrays[2 * row] = rays;
+                S.rowrays[2 * row + 1] = erays;
+                if (err) {
+                    atomicExch(&S.ctl[3], 1u);
+                    atomicExch(&S.ctl[1], 1u);
+                }
+                __threadfence();
+                atomicAdd(&S.ctl[0], 1u);
+            }
+        }
+        const uint64_t mv = wballot(moved);
+        if (lane_id() == 0 && mv) atomicAdd(&S.ctl[2], 1u);
+        ++n_sweep;
+        if (!wany(!done)) break;
+        if (rss_ld32(&S.ctl[1]) != 0u) break;  // aborted
+        if (!mv) __builtin_amdgcn_s_sleep(8);
+    }
+    if (mine) {
+        atomicAdd(&S.ctl[8], n_wait);
+        atomicAdd(&S.ctl[9], n_ext);
+        atomicAdd(&S.ctl[10], n_pre);
+    }
+    if (lane_id() == 0) atomicAdd(&S.ctl[11], n_sweep);
+}
+
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int OCC = 1, int TAIL = 0, int PROF = 0,
           int HELP = 0, int SAMP = 0>
@@ -700,9 +880,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                                                 unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
-    // SAMP 3 (shadow-free speculation): no light terms, no pending next ray
-    __shared__ float s_light[SAMP == 3 ? 1 : kMaxDepth * BLOCK];
-    __shared__ float s_next[SAMP == 3 ? 1 : 6 * BLOCK];
+    // SAMP 3, 4 (shadow-free speculation): no light terms, no pending next ray
+    __shared__ float s_light[SAMP >= 3 ? 1 : kMaxDepth * BLOCK];
+    __shared__ float s_next[SAMP >= 3 ? 1 : 6 * BLOCK];
+    if (SAMP == 4 && (int)blockIdx.x < pc.rss.nchase) {  // the streaming row engine's chasers
+        rss_chaser<BLOCK>(a, pc.rss, (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64));
+        return;
+    }
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
     constexpr uint32_t LS = BLOCK;  // stride between a lane's LDS entries
@@ -738,11 +922,18 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     const uint64_t lt = (1ull << lane_id()) - 1ull;
     uint32_t seg = (uint32_t)(gtid >> 6) % kSeg, walked = 0;
     uint32_t res = 0, res_end = 0;
-    if (SAMP >= 2) {  // the speculative row engine plans its units on the device
+    if (SAMP == 2 || SAMP == 3) {  // the speculative row engine plans its units on the device
         pc.P = *pc.p_dev;
         pc.nchunks = (uint32_t)((pc.P + pc.chunk - 1) / pc.chunk);
     }
-    bool exhausted = pc.P == 0;
+    bool exhausted = SAMP == 4 ? false : pc.P == 0;
+    // SAMP 4: the row the wave takes units from (it moves on when that row has
+    // none), the row and pixel of its reservation, the watchdog's last seen
+    // chain progress and when it changed
+    uint32_t crow = SAMP == 4 ? (uint32_t)((gtid >> 6) % (int64_t)max(1, pc.rss.nrows)) : 0u;
+    uint32_t srow = 0, spx = 0, wd_tick = 0, n_claim = 0, n_miss = 0, n_cas = 0;  // (ctl[5..7])
+    uint32_t crow_rng = (uint32_t)(gtid >> 6) * 2654435761u + 1u;
+    uint64_t wd_time = 0;
     if (kFull && pc.simd_reg && !exhausted) {  // SIMD-balanced first chunk
         const uint2 rd = simd_rank(pc.simd_reg);
         if (rd.x < pc.wps && rd.y < pc.nsimd) {
@@ -821,8 +1012,74 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             f3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
             // ---- new pixels for idle lanes (wave-uniform reservation)
             const uint64_t nopix = wballot(!has_pix && !(HELP && helper) && !exhausted);
+            if (SAMP == 4 && nopix != 0 && res >= res_end && !exhausted) {
+                // offsets of one pixel window, as many as the wave has idle
+                // lanes (a held reservation would delay units the chain may be
+                // waiting for): the row's demand window first, then its live
+                // windows in pixel order.  Lane i < T reads slot i, lane T the
+                // demand slot; the pick takes its offsets with one fetch-add,
+                // and the word it returns says which window they belong to
+                // (the chaser may have re-planned the slot meanwhile), so no
+                // offset handed out is ever lost; adds past a window's end
+                // hand out nothing.
+                const RsStream& S = pc.rss;
+                const uint32_t T = (uint32_t)kRssT;
+                // a wave with lanes still tracing looks at 1 row per round, an idle one at 4
+                const int natt = wany(has_pix) ? 1 : 4;
+                for (int att = 0; att < natt && res >= res_end; ++att) {
+                    const uint32_t x = (uint32_t)(rss_ld(&S.chainpos[crow]) >> 32);
+                    bool moved_on = true;
+                    if (x < (uint32_t)a.W) {
+                        unsigned long long* sl = S.slots + (size_t)crow * (T + 1u);
+                        const uint32_t ln = (uint32_t)lane_id();
+                        unsigned long long w = 0;
+                        if (ln <= T) w = rss_ld(&sl[ln]);
+                        const uint32_t p1 = (uint32_t)(w >> 48), q = (uint32_t)(w >> 24) & kRssM24;
+                        const uint32_t hi = (uint32_t)w & kRssM24;
+                        const bool valid = ln <= T && p1 > x && p1 <= (uint32_t)a.W && q < hi;
+                        // priority: demand, then the lowest pixel; key unique per lane
+                        uint32_t key = valid ? (((ln == T ? 0u : p1 - x) << 4) | ln) : 0xFFFFFFFFu;
+                        // (over all 64 lanes: the pick must be wave-uniform)
+                        for (int off = 1; off < 64; off <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, off));
+                        if (key != 0xFFFFFFFFu) {
+                            moved_on = false;
+                            const int pick = (int)(key & 15u);
+                            uint32_t got = 0, gq = 0, gp = 0;
+                            if (ln == (uint32_t)pick) {
+                                const uint32_t n = min((uint32_t)__popcll(nopix), hi - q);
+                                const unsigned long long old = atomicAdd(&sl[ln], (unsigned long long)n << 24);
+                                const uint32_t op = (uint32_t)(old >> 48), oq = (uint32_t)(old >> 24) & kRssM24;
+                                const uint32_t ohi = (uint32_t)old & kRssM24;
+                                if (op != 0u && oq < ohi) {
+                                    got = min(n, ohi - oq);
+                                    gq = oq;
+                                    gp = op - 1u;
+                                }
+                            }
+                            got = (uint32_t)__shfl((int)got, pick);
+                            if (!got) ++n_cas;
+                            if (got) {
+                                ++n_claim;
+                                res = (uint32_t)__shfl((int)gq, pick);
+                                res_end = res + got;
+                                srow = crow;
+                                spx = (uint32_t)__shfl((int)gp, pick);
+                            }
+                        }
+                    }
+                    if (moved_on) {  // no work there: a pseudo-random next row spreads the waves
+                        ++n_miss;
+                        crow_rng ^= crow_rng << 13;
+                        crow_rng ^= crow_rng >> 17;
+                        crow_rng ^= crow_rng << 5;
+                        crow = crow_rng % (uint32_t)S.nrows;
+                    }
+                }
+                if (res >= res_end && (rss_ld32(&S.ctl[0]) >= (uint32_t)S.nrows || rss_ld32(&S.ctl[1]) != 0u))
+                    exhausted = true;  // every row's chain is done (or the launch aborted)
+            }
             if (nopix != 0) {
-                while (res >= res_end && !exhausted) {
+                while (SAMP != 4 && res >= res_end && !exhausted) {
                     // chunks of segment seg: seg, seg + kSeg, ...
                     const uint32_t c = seg < pc.nchunks ? (pc.nchunks - 1u - seg) / (uint32_t)kSeg + 1u : 0u;
                     uint32_t b = c;
@@ -849,10 +1106,17 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const uint32_t k = (uint32_t)__popcll(nopix & lt);
                 if (!has_pix && ((nopix >> lane_id()) & 1ull) && k < take) {
                     uint32_t smp0 = (uint32_t)a.smp_begin;
-                    if (SAMP >= 2) {  // speculative row seeding: one sample from a given state
+                    if (SAMP == 4) {  // streaming row engine: offset res + k of pixel spx of row srow
                         cur_unit = res + k;
-                        pix = pc.upix[cur_unit];
+                        pix = srow * (uint32_t)a.W + spx;
+                        re0 = rays_e;
+                        rs0 = rays_s;
+                    } else if (SAMP >= 2) {  // speculative row seeding: one sample from a given state
+                        cur_unit = res + k;
+                        // no unit arrays: the chain list's unit u is sample u % spp of tile pixel u / spp
+                        pix = pc.upix ? pc.upix[cur_unit] : cur_unit / (uint32_t)a.spp;
                         if (pc.uslot) smp0 = pc.uslot[cur_unit];
+                        else if (!pc.upix) smp0 = cur_unit - pix * (uint32_t)a.spp;
                         re0 = rays_e;
                         rs0 = rays_s;
                     } else if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
@@ -866,7 +1130,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     has_pix = true;
                     const int lr = (int)(pix / (uint32_t)a.W);
                     const int x = (int)(pix - (uint32_t)lr * (uint32_t)a.W);
-                    if (SAMP >= 2) {
+                    if (SAMP == 4) {
+                        rng = rss_state(pc.rss, (int)srow, cur_unit);
+                    } else if (SAMP >= 2) {
                         rng = pc.ustate[cur_unit];
                     } else if (!kFull || a.smp_begin == 0) {
                         rng = pixel_seed((uint32_t)x, (uint32_t)tile_row_to_y(a, lr), (uint32_t)a.W);
@@ -914,11 +1180,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const f3 pos = hit_pos(mk(ha.x, ha.y, ha.z), mk(ha.w, hb.x, hb.y), mk(hb.z, hb.w, hc.x),
                                                ts.bu, ts.bv);
                         const float lc = light_cosine(nrm, r.d);
-                        if (SAMP != 3) light[depth * LS] = lc;  // zeroed if occluded
+                        if (SAMP < 3) light[depth * LS] = lc;  // zeroed if occluded
                         f3 target = pos + nrm + rnd;
                         f3 nd = normalize(target - pos);
                         ++depth;
-                        if (SAMP != 3 && lc > 0.0f && !(SAMP == 2 && pc.rs_noshadow)) {
+                        if (SAMP < 3 && lc > 0.0f && !(SAMP == 2 && pc.rs_noshadow)) {
                             nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
                             nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
                             start = true;  // shadow query toward the light
@@ -944,7 +1210,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         color = sky(r.d);  // main.cpp:106-107
                         finish = true;
                     }
-                } else if (SAMP != 3) {  // shadow query of bounce depth-1
+                } else if (SAMP < 3) {  // shadow query of bounce depth-1
                     if (ts.best >= 0) light[(depth - 1) * LS] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
                         start = true;  // the scattered ray of that bounce
@@ -996,7 +1262,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     for (int kk = 0; kk < (int)depth; ++kk) pend |= light[kk * LS] < 0.0f;
                 waiting = pend;
                 if (!pend) {
-                    if (SAMP != 3)
+                    if (SAMP < 3)
                         for (int kk = (int)depth - 1; kk >= 0; --kk)
                             color = backward_step(color, light[kk * LS]);
                     if (SAMP == 2 && pc.sbuf) {  // a chain sample traced in full: k_resolve sums in order
@@ -1004,6 +1270,16 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
                                                     reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss +
                                                                                         (size_t)pix * pc.sb_sp)));
+                    } else if (SAMP == 4) {  // streaming row engine: the unit's word for the chaser
+                        const uint32_t draws = ndraw + 2u * depth;
+                        const uint32_t ne = rays_e - re0, nr = ne + rays_s - rs0;  // <= 10, <= 20
+                        const uint32_t row = pix / (uint32_t)a.W, p = pix - row * (uint32_t)a.W;
+                        if (draws > 0x3FFFu) atomicExch(&pc.rss.ctl[3], 2u);  // cannot happen: 8k disk tries
+                        const unsigned long long word =
+                            ((((unsigned long long)(p + 1u) << 24) | cur_unit) << 28) |
+                            (unsigned long long)(min(draws, 0x3FFFu) | (nr << 14) | (ne << 19));
+                        atomicMax(pc.rss.res + ((size_t)row * kRssT + p % kRssT) * pc.rss.R + (cur_unit & pc.rss.rmask),
+                                  word);
                     } else if (SAMP >= 2) {  // speculative row seeding: render_rowspec's chase consumes it
                         // draws: the camera's, and RandomUnitVector's 2 at each of the
                         // `depth` hits (main.cpp:71, drawn at the 10th hit too)
@@ -1098,6 +1374,21 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         }
         if (!wany(in_query)) {
             if (exhausted && !wany(has_pix)) break;
+            if (SAMP == 4 && !wany(has_pix)) {  // nothing to take yet: wait for the chasers
+                // watchdog: no chain progress anywhere for ~1 s means the
+                // chasers cannot run; abort (the host re-renders the frame
+                // with render_rowspec) rather than spin forever
+                const uint32_t tick = rss_ld32(&pc.rss.ctl[2]);
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+                if (tick != wd_tick || wd_time == 0) {
+                    wd_tick = tick;
+                    wd_time = now;
+                } else if (now - wd_time > 100000000ull) {
+                    if (lane_id() == 0) atomicExch(&pc.rss.ctl[1], 1u);
+                    exhausted = true;
+                }
+                __builtin_amdgcn_s_sleep(32);
+            }
             continue;
         }
         for (int k = 0; k < STEPS; ++k) {  // traversal rounds
@@ -1144,6 +1435,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 pt_t = t;
             }
         }
+    }
+    if (SAMP == 4 && lane_id() == 0) {
+        atomicAdd(&pc.rss.ctl[5], n_claim);
+        atomicAdd(&pc.rss.ctl[6], n_miss);
+        atomicAdd(&pc.rss.ctl[7], n_cas);
     }
     uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
     uint32_t nv = COUNT ? wave_sum(cnt.nodes) : 0u;
@@ -1449,6 +1745,118 @@ __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const
         rs.lpix[base + t] = upix[e.x];
         rs.lstate[base + t] = ustate[e.x];
         rs.lslot[base + t] = e.y;
+    }
+}
+
+// The same chase for the listing (shadow-free) pass, one wave per row: the
+// row's unit words are staged in LDS with coalesced loads first, so the
+// chain's walk -- one dependent read per chain sample -- runs on LDS latency
+// instead of a global round trip each (the one-thread-per-row kernel spent
+// ~3.6 us per chain sample there).  The chain's (unit, sample) pairs collect
+// in LDS and the wave copies them into the frame's list.  Rows with more
+// units than kChaseUnits walk from global memory; the host only picks this
+// kernel when a row's chain samples per iteration fit kChaseList.
+constexpr uint32_t kChaseUnits = 8192, kChaseList = 2048;
+__global__ void __launch_bounds__(64) k_rs_chase_lds(RenderArgs a, RowSpec rs, const float4* __restrict__ rs_out,
+                                                     const uint32_t* __restrict__ rs_end,
+                                                     const uint32_t* __restrict__ upix,
+                                                     const uint32_t* __restrict__ ustate)
+{
+    __shared__ uint32_t s_w[kChaseUnits];
+    __shared__ uint2 s_l[kChaseList];
+    __shared__ uint32_t s_n, s_base;
+    const int r = blockIdx.x;
+    const int rows = rs.nrows;
+    const uint32_t lane = threadIdx.x;
+    if (rs.win[r] == 0) return;  // row finished (block-uniform)
+    const uint32_t u0 = rs.offs[r], nu = rs.offs[r + 1] - u0;
+    const bool staged = nu <= kChaseUnits;
+    if (staged)
+        for (uint32_t i = lane; i < nu; i += 64) s_w[i] = __float_as_uint(rs_out[u0 + i].w);
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t k = rs.k[r], x = rs.x[r], pdraws = rs.pdraws[r], rays = rs.rays[r], erays = rs.erays[r];
+        uint32_t n = rs.win[r], nl = 0;
+        uint32_t j = 0, last = 0xFFFFFFFFu, lo = 0, wb = u0;
+        int i = 0;
+        while (j >= lo && j - lo < n) {
+            const uint32_t idx = wb + (j - lo);
+            const uint32_t w = staged ? s_w[idx - u0] : __float_as_uint(rs_out[idx].w);
+            const uint32_t draws = w & ((1u << kRsDrawBits) - 1u);
+            rays += (w >> kRsDrawBits) & 31u;
+            erays += w >> 28;
+            pdraws += draws;
+            s_l[nl++] = make_uint2(idx, k);
+            last = idx;
+            j += draws >> 1;
+            if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
+                rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
+                ++x;
+                k = 0;
+                pdraws = 0;
+                if (++i >= rs.nwin) break;
+                wb += n;
+                n = rs.win[i * rows + r];
+                lo = rs.ws[i * rows + r];
+                if (n == 0) break;
+            }
+        }
+        if (last != 0xFFFFFFFFu) rs.rng[r] = rs_end[last];  // the next sample's start state
+        if (k != 0) ++rs.short_win[r];
+        rs.k[r] = k;
+        rs.x[r] = x;
+        rs.pdraws[r] = pdraws;
+        rs.rays[r] = rays;
+        rs.erays[r] = erays;
+        s_n = nl;
+        s_base = nl ? atomicAdd(rs.lcount, nl) : 0u;
+    }
+    __syncthreads();
+    const uint32_t nl = s_n, base = s_base;
+    for (uint32_t t = lane; t < nl; t += 64) {
+        const uint2 e = s_l[t];
+        rs.lpix[base + t] = upix[e.x];
+        rs.lstate[base + t] = ustate[e.x];
+        rs.lslot[base + t] = e.y;
+    }
+}
+
+// render_rowstream: each row's anchor states M^(2^15 a) row_seed, a < na, from
+// the byte tables of M^(2^15 a0) (j1) and M^(2^20 a1) (j2), a = 32 a1 + a0;
+// thread 0 also publishes the final pass's unit count.
+__global__ void __launch_bounds__(256) k_rss_anchors(RenderArgs a, RsStream S, const uint32_t* __restrict__ j1,
+                                                     const uint32_t* __restrict__ j2)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) S.ctl[4] = (uint32_t)((size_t)a.slots * (size_t)a.spp);
+    if (i >= (size_t)S.nrows * S.na) return;
+    const int row = (int)(i / S.na);
+    const uint32_t an = (uint32_t)(i - (size_t)row * S.na);
+    const uint32_t seed = row_seed((uint32_t)tile_row_to_y(a, row));  // main.cpp:204, unmodified
+    const_cast<uint32_t*>(S.anchors)[i] = sample_seed(j2, an >> 5, sample_seed(j1, an & 31u, seed));
+}
+
+// The chain list's offsets -> start states, in place (unit u: row u / spp / W).
+__global__ void __launch_bounds__(256) k_rss_states(RenderArgs a, RsStream S)
+{
+    const size_t u = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= (size_t)a.slots * (size_t)a.spp) return;
+    const int row = (int)(u / ((size_t)a.spp * (size_t)a.W));
+    S.list[u] = rss_state(S, row, S.list[u]);
+}
+
+// The chain rays of render_rowstream's rows: counters[0] all, [3] closest-hit.
+__global__ void __launch_bounds__(256) k_rss_count(RsStream S, unsigned long long* counters)
+{
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    unsigned long long sv = r < S.nrows ? S.rowrays[2 * r] : 0u, se = r < S.nrows ? S.rowrays[2 * r + 1] : 0u;
+    for (int off = 32; off > 0; off >>= 1) {
+        sv += __shfl_xor(sv, off);
+        se += __shfl_xor(se, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&counters[0], sv);
+        atomicAdd(&counters[3], se);
     }
 }
 
@@ -1994,6 +2402,198 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     return 0;
 }
 
+// Streaming row engine (RsStream above): one k_path<SAMP 4> launch whose first
+// blocks chase the rows' chains while the rest trace the windows' units, then
+// the chain's samples in full (k_path<SAMP 2> over the chain list) and the
+// in-order sums (k_resolve_px).  Returns 1 when it does not apply (limits,
+// memory) or the launch aborted (its watchdog: no chain progress for ~1 s),
+// and the caller runs render_rowspec instead.
+int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
+{
+    const Options& o = s.opt;
+    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
+    auto fn2 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
+    auto fn4 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
+    const int rows = a.tile_rows;
+    const uint32_t W = (uint32_t)a.W, spp = (uint32_t)a.spp, T = (uint32_t)kRssT;
+    const size_t lcap = (size_t)a.slots * spp;  // chain samples of the tile
+    // a pixel's offsets per window ~ spp x 8.5 (draws / 2); the ring holds the
+    // live windows with room to spare (pow2 >= 16 x spp x 8)
+    uint32_t R = 1024;
+    while (R < 128u * spp) R <<= 1;
+    // offsets live in 24-bit fields: ~8.5 per sample on average, 14 allowed,
+    // plus 2^20 of room for the workers' fetch-adds past a window's end
+    if (rows < 1 || W > 4094u || (uint64_t)W * spp * 14u + R + (1u << 20) >= (1ull << 24) || lcap >= (1ull << 31))
+        return 1;
+    const int grid = occupancy_grid((const void*)fn4, kBlk, 0, s.device);
+    const int grid2 = occupancy_grid((const void*)fn2, kBlk, 0, s.device);
+    const int nchase = (rows + kBlk - 1) / kBlk;  // blocks of 4 waves x 64 rows
+    if (grid <= 2 * nchase) return 1;
+    // live windows per row: ~8 units per resident lane over the rows, 2..kRssT-1
+    const int64_t lanes = (int64_t)(grid - nchase) * kBlk;
+    const double E_est = (double)spp * 8.5;
+    int nw = (int)std::lround((double)lanes * 8.0 / ((double)rows * E_est));
+    nw = std::max(2, std::min(kRssT - 1, nw));
+    if (o.rowspec_windows > 0) nw = std::min(kRssT - 1, o.rowspec_windows);
+    const uint32_t na = (uint32_t)(((uint64_t)W * spp * 14u + R) >> 14) + 1u;
+    const size_t ovf_words = (size_t)std::max(grid, grid2) * kBlk * (kStackTotal - kPathSL);
+    const size_t head_words = (size_t)kSeg * kCtr;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_res = al((size_t)rows * T * R * 8), b_slots = al((size_t)rows * (T + 1) * 8),
+                 b_pos = al((size_t)rows * 8), b_rays = al((size_t)rows * 2 * 4), b_lo = al((size_t)rows * T * 4),
+                 b_ctl = al(64), b_ctr = al(24 * 8), b_anch = al((size_t)rows * na * 4),
+                 b_ovf = al((ovf_words + head_words) * 4);
+    const size_t zero_bytes = b_res + b_slots + b_pos + b_rays + b_lo + b_ctl + b_ctr;
+    const size_t need = zero_bytes + b_anch + b_ovf;
+    const size_t lneed = lcap * sizeof(uint32_t), sneed = lcap * sizeof(float4);
+    {
+        size_t fr = 0, tot = 0;
+        const size_t budget = (hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0) + s.rss_bytes +
+                              s.rs_list_bytes + s.sbuf_bytes;
+        if (need + lneed + sneed > budget) return 1;
+    }
+    auto grow = [](void*& p, size_t& have, size_t want) -> int {
+        if (have >= want) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        have = 0;
+        if (hipMalloc(&p, want) != hipSuccess) return -1;
+        have = want;
+        return 0;
+    };
+    if (grow(s.rss_buf, s.rss_bytes, need) || grow(s.rs_list, s.rs_list_bytes, lneed)) {
+        set_error("render_rowstream: out of device memory");
+        return -1;
+    }
+    {
+        void* sb = s.sbuf;
+        if (grow(sb, s.sbuf_bytes, sneed)) {
+            s.sbuf = nullptr;
+            set_error("render_rowstream: out of device memory");
+            return -1;
+        }
+        s.sbuf = static_cast<float4*>(sb);
+    }
+    if (!s.rss_tab) {  // M^(2c) and M^(256b) for c, b < 128; M^(2^15 a0), M^(2^20 a1) for a0, a1 < 32
+        std::vector<uint32_t> tab, t;
+        jump_tables(2, 128, t);
+        tab.insert(tab.end(), t.begin(), t.end());
+        jump_tables(256, 128, t);
+        tab.insert(tab.end(), t.begin(), t.end());
+        jump_tables(1ull << 15, 32, t);
+        tab.insert(tab.end(), t.begin(), t.end());
+        jump_tables(1ull << 20, 32, t);
+        tab.insert(tab.end(), t.begin(), t.end());
+        uint32_t* nt = nullptr;
+        TMPT_HIP(hipMalloc(&nt, tab.size() * sizeof(uint32_t)));
+        if (hipMemcpy(nt, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(nt);
+            set_error("render_rowstream: jump table upload failed");
+            return -1;
+        }
+        s.rss_tab = nt;
+    }
+    if (!s.rss_host) TMPT_HIP(hipHostMalloc((void**)&s.rss_host, 16 * sizeof(uint32_t), hipHostMallocDefault));
+    char* p = static_cast<char*>(s.rss_buf);
+    RsStream S;
+    memset(&S, 0, sizeof(S));
+    S.res = reinterpret_cast<unsigned long long*>(p);
+    p += b_res;
+    S.slots = reinterpret_cast<unsigned long long*>(p);
+    p += b_slots;
+    S.chainpos = reinterpret_cast<unsigned long long*>(p);
+    p += b_pos;
+    S.rowrays = reinterpret_cast<uint32_t*>(p);
+    p += b_rays;
+    S.lo = reinterpret_cast<uint32_t*>(p);
+    p += b_lo;
+    S.ctl = reinterpret_cast<uint32_t*>(p);
+    p += b_ctl;
+    unsigned long long* spec_ctr = reinterpret_cast<unsigned long long*>(p);  // traced (not chain) rays
+    p += b_ctr;
+    S.anchors = reinterpret_cast<uint32_t*>(p);
+    p += b_anch;
+    uint32_t* ovf = reinterpret_cast<uint32_t*>(p);
+    uint32_t* heads = ovf + ovf_words;
+    S.list = static_cast<uint32_t*>(s.rs_list);
+    S.t1 = s.rss_tab;
+    S.t2 = s.rss_tab + 128 * 1024;
+    S.na = na;
+    S.jlimit = na << 14;
+    S.R = R;
+    S.rmask = R - 1u;
+    S.nrows = rows;
+    S.nchase = nchase;
+    S.nw = nw;
+    // window spread in pixels (render_rowspec's rule for its window count)
+    S.spread = o.rowspec_spread >= 0.0f ? o.rowspec_spread : 0.07f + 0.016f * (float)nw;
+    TMPT_HIP(hipMemsetAsync(s.rss_buf, 0, zero_bytes, s.stream));
+    {
+        const size_t n = (size_t)rows * na;
+        k_rss_anchors<<<(unsigned)((n + 255) / 256), 256, 0, s.stream>>>(a, S, s.rss_tab + 256 * 1024,
+                                                                        s.rss_tab + 288 * 1024);
+        TMPT_HIP(hipGetLastError());
+    }
+    RenderArgs as = a;
+    as.jt = nullptr;
+    as.bmask = 0u;  // every unit is one sample
+    as.smp_begin = 0;
+    as.smp_end = a.spp;
+    PathCtl pc;
+    memset(&pc, 0, sizeof(pc));
+    pc.heads = heads;
+    pc.nblk = pc.blk = 1u;
+    pc.lane_cap = 64u;
+    pc.chunk = kChunk;
+    pc.rs_noshadow = 1;
+    pc.rss = S;
+    fn4<<<grid, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, ovf, spec_ctr);
+    TMPT_HIP(hipGetLastError());
+    TMPT_HIP(hipMemcpyAsync(s.rss_host, S.ctl, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+    TMPT_HIP(hipStreamSynchronize(s.stream));
+    if (s.rss_host[1] != 0u || s.rss_host[3] != 0u || s.rss_host[0] != (uint32_t)rows) {
+#ifdef TMPT_DIAG
+        fprintf(stderr, "rowstream: aborted (rows done %u of %d, abort %u, error %u); iterated engine instead\n",
+                s.rss_host[0], rows, s.rss_host[1], s.rss_host[3]);
+#endif
+        return 1;
+    }
+    // the chain's samples in full (shadows included), then the in-order sums
+    k_rss_states<<<(unsigned)((lcap + 255) / 256), 256, 0, s.stream>>>(a, S);
+    PathCtl pc2 = pc;
+    pc2.upix = nullptr;  // unit u = sample u % spp of tile pixel u / spp
+    pc2.uslot = nullptr;
+    pc2.ustate = S.list;
+    pc2.p_dev = S.ctl + 4;
+    pc2.rs_noshadow = 0;
+    pc2.sbuf = s.sbuf;
+    pc2.sb_ss = 1u;
+    pc2.sb_sp = spp;
+    TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
+    fn2<<<grid2, kBlk, 0, s.stream>>>(view(s), as, pc2, d_out, ovf, spec_ctr + 16);
+    k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(s.sbuf, a.slots, a.spp, a.spp_recip, d_out);
+    k_rss_count<<<(unsigned)((rows + 255) / 256), 256, 0, s.stream>>>(S, d_counters);
+    TMPT_HIP(hipGetLastError());
+    s.path_launches = 1;
+#ifdef TMPT_DIAG
+    if (getenv("TMPT_ROWSPEC_LOG")) {
+        unsigned long long c[2] = {0, 0}, t = 0;
+        TMPT_HIP(hipMemcpyAsync(c, d_counters, sizeof(c), hipMemcpyDeviceToHost, s.stream));
+        TMPT_HIP(hipMemcpyAsync(&t, spec_ctr, sizeof(t), hipMemcpyDeviceToHost, s.stream));
+        TMPT_HIP(hipStreamSynchronize(s.stream));
+        fprintf(stderr,
+                "rowstream: %d rows, %d worker blocks + %d chaser blocks, ring %u, %d windows, traced rays %llu for "
+                "%llu chain rays (x%.2f), chain ticks %u\n"
+                "rowstream: claims %u, row misses %u, lost CAS %u; chaser waits %u, extensions %u, prefixes %u, "
+                "sweeps %u\n",
+                rows, grid - nchase, nchase, R, nw, t, c[0], c[0] ? (double)t / (double)c[0] : 0.0, s.rss_host[2],
+                s.rss_host[5], s.rss_host[6], s.rss_host[7], s.rss_host[8], s.rss_host[9], s.rss_host[10],
+                s.rss_host[11]);
+    }
+#endif
+    return 0;
+}
+
 // Speculative row seeding (k_rs_* above): iterations of plan -> fill ->
 // k_path<SAMP 2> -> chase until every row of the tile has its W pixels.  Each
 // iteration moves every unfinished row through (usually) one pixel.  The rows
@@ -2214,6 +2814,10 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         k_rs_init<<<(unsigned)((q.rs.nrows + 255) / 256), 256, 0, q.st>>>(a, q.rs);
     }
     TMPT_HIP(hipGetLastError());
+    // the listing pass's chase walks in LDS (one wave per row) when a row's
+    // chain samples of one iteration fit its list; option rowspec_chase 0 = the
+    // one-thread-per-row kernel
+    const bool chase_lds = noshadow && o.rowspec_chase != 0 && (uint64_t)nwin * (uint64_t)a.spp <= kChaseList;
     int it = 0;
     // every iteration moves each unfinished row by >= 1 sample, so W * spp bounds them
     const int64_t max_it = (int64_t)a.W * a.spp + kCheck;
@@ -2226,8 +2830,12 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
                 TMPT_HIP(hipMemsetAsync(q.heads, 0, head_words * 4, q.st));
                 if (noshadow) fn3<<<pgrid3, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
                 else fn<<<pgrid, kBlk, 0, q.st>>>(view(s), as, q.pc, d_out, q.ovf, spec_ctr);
-                k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, d_out,
-                                                                                q.upix, q.ustate);
+                if (chase_lds)
+                    k_rs_chase_lds<<<(unsigned)q.rs.nrows, 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end, q.upix,
+                                                                         q.ustate);
+                else
+                    k_rs_chase<<<(unsigned)((q.rs.nrows + 63) / 64), 64, 0, q.st>>>(a, q.rs, q.rs_out, q.rs_end,
+                                                                                    d_out, q.upix, q.ustate);
             }
         TMPT_HIP(hipGetLastError());
         // the last plan of each group: 0 units = the group was already done
@@ -2410,7 +3018,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
-        else if (rowspec) rc = render_rowspec(s, a, d_out, d_counters);
+        else if (rowspec) {
+            // the streaming engine, or the iterated one where it does not apply
+            rc = s.opt.rowspec_stream != 0 && s.opt.rowspec_noshadow != 0 ? render_rowstream(s, a, d_out, d_counters)
+                                                                          : 1;
+            if (rc == 1) rc = render_rowspec(s, a, d_out, d_counters);
+        }
         else rc = render_megakernel(s, a, d_out, count, d_counters);
     }
     (void)hipEventRecord(e1, s.stream);
