@@ -15,8 +15,19 @@ shards = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 os.environ["TMPT_ROUND_LOG"] = "1"
 tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
 cam = tm.Camera.for_scene(bmin, bmax, 1920, 1080, is_sponza=True)
+# optional third argument: render-option variants for sample seeding, "defer=0;defer=1"
+variants = sys.argv[3].split(";") if len(sys.argv) > 3 else None
+runs = [("pixel", tm.SEED_PIXEL, ""), ("sample", tm.SEED_SAMPLE, "")] if variants is None else \
+    [("sample " + v, tm.SEED_SAMPLE, v) for v in variants]
 with tm.Scene(tris) as sc:
-    for name, seed in (("pixel", tm.SEED_PIXEL), ("sample", tm.SEED_SAMPLE)):
+    defaults = {}
+    for name, seed, v in runs:
+        for k, val in defaults.items():
+            sc.set_option(k, val)
+        for kv in filter(None, v.split("&")):
+            k, _, val = kv.partition("=")
+            defaults.setdefault(k, sc.get_option(k))
+            sc.set_option(k, float(val))
         print(f"--- {name} seeding, {spp} spp, shard 0 of {shards}", file=sys.stderr, flush=True)
         _, rays = sc.trace_image(cam, 1920, 1080, spp, seed_mode=seed, band_rows=1, num_shards=shards,
                                  count_visits=True)
