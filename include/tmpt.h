@@ -175,7 +175,8 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    shadow-free speculation + one full re-trace (1), the
  *                    chase over LDS-staged units, one wave per row (1), the
  *                    streaming engine: one launch, chains walked on the device
- *                    as units finish (1; 0 = host-driven iterations, the default)
+ *                    as units finish (1, the default; 0 = host-driven iterations,
+ *                    also the fallback when the streaming engine does not apply)
  *   wf_bins          wavefront engine: each segment's extend queue split by the
  *                    rays' direction octant into 1, 2, 4 or 8 sub-queues (1) */
 int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);

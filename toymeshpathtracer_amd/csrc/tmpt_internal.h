@@ -94,7 +94,7 @@ struct Options {
     int rowspec_groups = 2;   // row seeding: row groups on their own streams
     int rowspec_noshadow = 1; // row seeding: shadow-free speculation + one full re-trace of the chain
     int rowspec_chase = 1;    // row seeding, shadow-free: the chase walks LDS-staged units, one wave per row
-    int rowspec_stream = 0;   // row seeding: the streaming row engine (one launch; 0 = iterations)
+    int rowspec_stream = 1;   // row seeding: the streaming row engine (one launch; 0 = iterations)
     int wf_bins = 1;          // wavefront engine: extend sub-queues per segment by direction octant (1, 2, 4, 8)
 };
 int options_parse(Options& o, const char* text, bool allow_build);

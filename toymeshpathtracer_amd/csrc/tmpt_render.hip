@@ -2429,10 +2429,13 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     const int grid2 = occupancy_grid((const void*)fn2, kBlk, 0, s.device);
     const int nchase = (rows + kBlk - 1) / kBlk;  // blocks of 4 waves x 64 rows
     if (grid <= 2 * nchase) return 1;
-    // live windows per row: ~8 units per resident lane over the rows, 2..kRssT-1
+    // live windows per row: 1.5 + 0.8 x (resident lanes per pixel window of
+    // all rows), 2..kRssT-1.  Bench frame, 64 spp (profiles/r03_rowspec/):
+    // best 2 windows at N = 1 and 1/2 (2.03 s, 1.08 s), 3-4 at 1/4 (0.65 s),
+    // 4-7 at 1/8 (0.48 s); this rule picks 2, 2, 3, 5
     const int64_t lanes = (int64_t)(grid - nchase) * kBlk;
     const double E_est = (double)spp * 8.5;
-    int nw = (int)std::lround((double)lanes * 8.0 / ((double)rows * E_est));
+    int nw = (int)std::lround(1.5 + 0.8 * (double)lanes / ((double)rows * E_est));
     nw = std::max(2, std::min(kRssT - 1, nw));
     if (o.rowspec_windows > 0) nw = std::min(kRssT - 1, o.rowspec_windows);
     const uint32_t na = (uint32_t)(((uint64_t)W * spp * 14u + R) >> 14) + 1u;
