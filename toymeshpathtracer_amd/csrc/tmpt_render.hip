@@ -2429,13 +2429,15 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     const int grid2 = occupancy_grid((const void*)fn2, kBlk, 0, s.device);
     const int nchase = (rows + kBlk - 1) / kBlk;  // blocks of 4 waves x 64 rows
     if (grid <= 2 * nchase) return 1;
-    // live windows per row: 1.5 + 0.8 x (resident lanes per pixel window of
-    // all rows), 2..kRssT-1.  Bench frame, 64 spp (profiles/r03_rowspec/):
-    // best 2 windows at N = 1 and 1/2 (2.03 s, 1.08 s), 3-4 at 1/4 (0.65 s),
-    // 4-7 at 1/8 (0.48 s); this rule picks 2, 2, 3, 5
+    // live windows per row: 2.6 + 1.5 ln(room), room = resident lanes per
+    // pixel window of all rows, within 2..kRssT-1.  Bench frame, 64 spp
+    // (profiles/r03_rowspec/stream_windows_*, with the spread rule below):
+    // best 2 windows at N = 1 (1.82 s), 3 at 1/2 (1.05 s), 4 at 1/4 (0.65 s),
+    // 4-5 at 1/8 (0.44 s); this rule picks 2, 3, 4, 5
     const int64_t lanes = (int64_t)(grid - nchase) * kBlk;
     const double E_est = (double)spp * 8.5;
-    int nw = (int)std::lround(1.5 + 0.8 * (double)lanes / ((double)rows * E_est));
+    const double room = (double)lanes / ((double)rows * E_est);  // resident lanes per pixel window of all rows
+    int nw = (int)std::lround(2.6 + 1.5 * std::log(std::max(room, 1e-3)));
     nw = std::max(2, std::min(kRssT - 1, nw));
     if (o.rowspec_windows > 0) nw = std::min(kRssT - 1, o.rowspec_windows);
     const uint32_t na = (uint32_t)(((uint64_t)W * spp * 14u + R) >> 14) + 1u;
@@ -2528,8 +2530,13 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     S.nrows = rows;
     S.nchase = nchase;
     S.nw = nw;
-    // window spread in pixels (render_rowspec's rule for its window count)
-    S.spread = o.rowspec_spread >= 0.0f ? o.rowspec_spread : 0.07f + 0.016f * (float)nw;
+    // window spread in pixels: 0.055 x room - 0.015, within 0..0.25.  Bench
+    // frame, 64 spp (profiles/r03_rowspec/stream_spread_*): best at 0 - 0.02
+    // for N = 1 (1.82 s; 2.03 s at the earlier 0.10), 0.06 - 0.08 at 1/2, 0.12 -
+    // 0.15 at 1/4, 0.18 - 0.22 at 1/8 (0.44 s); at full load the chaser's demand
+    // and extension windows are cheaper than a wide spread
+    S.spread = o.rowspec_spread >= 0.0f ? o.rowspec_spread
+                                        : (float)std::min(0.25, std::max(0.0, 0.055 * room - 0.015));
     TMPT_HIP(hipMemsetAsync(s.rss_buf, 0, zero_bytes, s.stream));
     {
         const size_t n = (size_t)rows * na;
