@@ -31,9 +31,13 @@ def main():
     tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=True)
     sc = tm.Scene(tris)
-    defaults = {k: sc.get_option(k) for k in ("rowspec", "rowspec_wmax", "rowspec_windows", "rowspec_spread",
-                                              "rowspec_groups", "rowspec_noshadow", "rowspec_chase",
-                                              "rowspec_stream")}
+    defaults = {}
+    for k in ("rowspec", "rowspec_wmax", "rowspec_windows", "rowspec_spread", "rowspec_groups", "rowspec_noshadow",
+              "rowspec_chase", "rowspec_stream"):
+        try:  # an older library build (TMPT_LIB_PATH) may not know every option
+            defaults[k] = sc.get_option(k)
+        except tm.TmptError:
+            pass
     ref = None
     res = {v: [] for v in variants}
     for _ in range(rounds):
