@@ -48,10 +48,14 @@ def parse(v):
 
 scenes = {}
 with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after each variant
-    DEFAULTS = {k: _probe.get_option(k) for k in ("sample_block", "sbuf_max", "pilot", "help", "pair", "balance", "dprio",
-                                                  "wave_cap", "rowspec", "rowspec_wmax", "rowspec_windows",
-                                                  "rowspec_spread", "rowspec_groups", "rowspec_noshadow", "rowspec_chase", "rowspec_stream",
-                                                  "wf_bins")}
+    DEFAULTS = {}
+    for _k in ("sample_block", "sbuf_max", "pilot", "help", "pair", "balance", "dprio", "wave_cap", "rowspec",
+               "rowspec_wmax", "rowspec_windows", "rowspec_spread", "rowspec_groups", "rowspec_noshadow",
+               "rowspec_chase", "rowspec_stream", "wf_bins"):
+        try:  # an older library build (TMPT_LIB_PATH) may not know every option
+            DEFAULTS[_k] = _probe.get_option(_k)
+        except tm.TmptError:
+            pass
 
 
 def scene_for(env):
