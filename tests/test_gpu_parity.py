@@ -252,6 +252,21 @@ def test_rowspec_equals_row_chains(gpu, name, w, h, spp, opts):
     sc.close()
 
 
+def test_rowstream_fallback_wide_rows(gpu):
+    """Rows wider than the streaming engine's limit (W > 4094: its 12-bit
+    window fields) take the iterated engine instead: the same image and rays
+    as the one-lane-per-row chains, and the iterated engine ran (more than one
+    iteration)."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    w, h, spp = 4100, 3, 2
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
+    b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    assert sc.stats().iterations > 1
+    assert ra == rb and np.array_equal(a, b)
+    sc.close()
+
+
 def test_rowspec_shards_and_oracle(gpu):
     """Row seeding over 3 interleaved shards (each row's chain is independent):
     the tiles reassemble to the 1-shard frame, which equals the oracle's row
