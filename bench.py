@@ -21,6 +21,13 @@ run by the speculative row engine.  All three are byte-exact against their
 oracle legs (tests/); the line also reports the other modes' throughput
 (seed_modes), timed the same way after the main run.
 
+Launch: `python bench.py --gpus N` with N > 1 and no launcher around it (no
+WORLD_SIZE in the environment) starts N ranks itself -- this process runs
+`torch.distributed.run` as a child before it has touched the GPU, and exits
+with its code -- after checking that N GPUs are visible (nccl; the gloo
+rehearsal may put several ranks on one GPU).  Under a launcher, WORLD_SIZE must
+equal --gpus.
+
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
   roofline      dominant kernel (k_path: all queries of the frame), its mean
                 launch time HIP-event timed on the stream it runs on, against
@@ -42,12 +49,69 @@ import argparse
 import contextlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "data"))
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="sponza1080", choices=["sponza1080", "teapot720", "suzanne360", "sponza4k"])
+    ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
+    ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel", "row"])
+    ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding modes")
+    ap.add_argument("--compare", action="store_true",
+                    help="time the other seeding modes at N>1 too (default: only at N=1, so the driver's "
+                         "multi-GPU runs are not slowed)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the collective path (process group, gather, max-over-ranks) even at one rank "
+                         "(tests the RCCL calls on a 1-GPU box)")
+    ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline: time budget of the row sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--save", default="", help="rank 0 writes the frame as PNG here")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path "
+                         "(ranks may share one GPU)")
+    return ap.parse_args(argv)
+
+
+def launch_ranks_if_needed() -> None:
+    """--gpus N without a launcher: run N ranks under torch.distributed.run (a
+    child process; this one has made no GPU call -- counting devices does not
+    initialise them -- and exits with the child's code).  Fails loudly when
+    nccl would need more GPUs than are visible."""
+    args = parse_args()
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return
+    import torch
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL (one rank per GPU); "
+              f"{ndev} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if ndev < 1:
+        print("bench.py: no GPU visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    sys.exit(subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode)
+
+
+if __name__ == "__main__":
+    launch_ranks_if_needed()
 
 import numpy as np  # noqa: E402
 
@@ -250,34 +314,16 @@ def stdout_to_stderr():
 
 
 def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="sponza1080", choices=sorted(CONFIGS))
-    ap.add_argument("--engine", default="persistent", choices=["wavefront", "persistent", "mega"])
-    ap.add_argument("--seed-mode", default="sample", choices=["sample", "pixel", "row"])
-    ap.add_argument("--no-compare", action="store_true", help="skip timing the other seeding modes")
-    ap.add_argument("--compare", action="store_true",
-                    help="time the other seeding modes at N>1 too (default: only at N=1, so the driver's "
-                         "multi-GPU runs are not slowed)")
-    ap.add_argument("--force-dist", action="store_true",
-                    help="run the collective path (process group, gather, max-over-ranks) even at one rank "
-                         "(tests the RCCL calls on a 1-GPU box)")
-    ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented run")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline: time budget of the row sample")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--save", default="", help="rank 0 writes the frame as PNG here")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path "
-                         "(ranks may share one GPU)")
-    args = ap.parse_args()
+    args = parse_args()
+    assert set(CONFIGS) == {"sponza1080", "teapot720", "suzanne360", "sponza4k"}
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        # measuring another GPU count than asked for would mislabel the line
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world} (the launcher started {world} ranks)")
+        sys.exit(2)
     dist_on = world > 1 or args.force_dist  # the collective path (process group, gather, reductions)
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1) if args.dist_backend == "gloo" else local
@@ -302,7 +348,9 @@ def main() -> None:
     tris, bmin, bmax = tm.load_scene(path)
     cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
     t0 = time.perf_counter()
-    scene = tm.Scene(tris, device=local)
+    # Scene + BuildOctree (main.cpp:165, 312): the BVH on the device, and the
+    # reference's octree for the queries it decides (ties on t, its root box)
+    scene = tm.Scene(tris, device=local, bounds=(bmin, bmax))
     init_s = time.perf_counter() - t0
     st0 = scene.stats()
 
@@ -340,8 +388,11 @@ def main() -> None:
     ext_ms = sh_ms = 0.0
     ext_rays = sh_rays = 0
     ext_launches = 0
+    ties = roots = 0
     for _ in range(args.steps):
         r, st = step()
+        ties += st.tie_queries
+        roots += st.root_misses
         rays += r
         ext_ms += st.extend_ms
         sh_ms += st.shadow_ms
@@ -492,6 +543,12 @@ def main() -> None:
         "bvh": {"lbvh2_depth": st0.bvh_depth, "bvh4_nodes": st0.bvh4_nodes, "bvh4_depth": st0.bvh4_depth,
                 "leaf_max": st0.leaf_max, "builder": "ploc" if st0.builder_iters else "lbvh",
                 "ploc_iters": st0.builder_iters},
+        # the reference's octree (scene.cpp:99-160, host-built) answers the
+        # closest hits whose t two or more triangles share, in its visit order
+        "reference_octree": {"nodes": st0.octree_nodes, "leaves": st0.octree_leaves, "refs": st0.octree_refs,
+                             "build_ms": round(st0.octree_build_ms, 1), "tie_rule": "visit" if st0.tie_rule == 0 else "index",
+                             "tie_queries_per_step": ties // max(args.steps, 1),
+                             "root_misses_per_step": roots // max(args.steps, 1)},
     }
     print(json.dumps(out), flush=True)
     scene.close()

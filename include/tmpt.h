@@ -22,13 +22,17 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 6  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+#define TMPT_ABI_VERSION 7  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
                               4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
                               progressive continuation keyed on the camera,
                               TMPT_SEED_SAMPLE; 6: scene options (tmpt_scene_create_ex,
                               tmpt_scene_set_option / get_option) replace the
                               library's environment variables, tmpt_scene_hit_ranged
-                              (per-ray tmin / tmax), tmpt_render_multi gathers over RCCL */
+                              (per-ray tmin / tmax), tmpt_render_multi gathers over RCCL;
+                              7: tmpt_scene_build_octree (the reference's octree: its answer
+                              for closest hits tied on t and for rays its root box drops),
+                              option tie_rule, tmpt_octree_digest, tmpt_stats octree / tie /
+                              row-engine fields, tmpt_render_multi takes the octree box */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -112,6 +116,20 @@ typedef struct {
     double build_ms;                 /* LBVH build of the scene */
     int32_t bvh_nodes, bvh_depth, n_tris, device;
     int32_t bvh4_nodes, bvh4_depth, leaf_max, builder_iters; /* 4-wide tree; PLOC passes (0 = LBVH) */
+    /* the reference's octree (tmpt_scene_build_octree; 0 when none) */
+    int32_t octree_nodes, octree_leaves;
+    int64_t octree_refs;             /* triangle references in its leaves */
+    double octree_build_ms;          /* host build */
+    /* the last render or HitScene call: closest-hit queries whose t two or more
+     * triangles share, answered again in the octree's visit order; and queries
+     * the reference's root box test rejected (answered as misses) */
+    uint64_t tie_queries, root_misses;
+    int32_t row_engine;       /* last render in row seeding: 0 none, 1 one lane per row (megakernel),
+                                 2 iterated speculative engine, 3 streaming speculative engine */
+    int32_t stream_fallbacks; /* 1: the streaming engine's launch aborted (no chain progress) and the
+                                 frame was rendered again by the iterated engine */
+    int32_t octree_depth;
+    int32_t tie_rule;         /* in effect: 0 octree visit order, 1 lowest index (no octree / option) */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */
@@ -136,8 +154,8 @@ int tmpt_camera_for_scene(tmpt_camera* cam, const float bmin[3], const float bma
 
 int tmpt_device_count(void);
 
-/* Scene::Scene (scene.h:19, scene.cpp:97-100) + Scene::BuildOctree
- * (scene.h:26, scene.cpp:118-126): copies n triangles (n*9 floats, v0 v1 v2)
+/* Scene::Scene (scene.h:19, scene.cpp:54-57) + Scene::BuildOctree
+ * (scene.h:26, scene.cpp:75-83): copies n triangles (n*9 floats, v0 v1 v2)
  * to `device` and builds the BVH there.  The caller keeps ownership of tris.
  * tmpt_scene_create = tmpt_scene_create_ex with no options. */
 int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene** out);
@@ -145,7 +163,7 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
 /* Scene options: the library's whole control plane (no environment variables;
  * the reference has no counterpart -- its constants are compiled in).  Every
  * option has a default that reproduces the measured-best configuration; all of
- * them change speed, never the image or the HitScene answers.
+ * them change speed, never the image or the HitScene answers (tie_rule aside).
  * `options` = "key=value,key=value" (NULL or "" = defaults); an unknown key or
  * a value out of range is an error (-22).
  * Build options (only at creation):
@@ -177,15 +195,43 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    streaming engine: one launch, chains walked on the device
  *                    as units finish (1, the default; 0 = host-driven iterations,
  *                    also the fallback when the streaming engine does not apply)
+ *   rowstream_test_abort  test hook (0): 1 makes the streaming engine's chaser
+ *                    blocks leave at once, so its watchdog (~2 ms then, ~1 s
+ *                    normally) aborts the launch and the iterated engine renders
+ *                    the frame -- the abort-and-fallback path, reported in
+ *                    tmpt_stats.stream_fallbacks
  *   wf_bins          wavefront engine: each segment's extend queue split by the
- *                    rays' direction octant into 1, 2, 4 or 8 sub-queues (1) */
+ *                    rays' direction octant into 1, 2, 4 or 8 sub-queues (1)
+ *   tie_rule         visit (0, default) | index (1): closest hits tied on t take the
+ *                    reference's octree visit order (needs tmpt_scene_build_octree)
+ *                    or the lowest triangle index -- the one option that can change
+ *                    an answer, by design: index is the exact-semantics contract */
 int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);
 int tmpt_scene_set_option(tmpt_scene* scene, const char* key, double value);
 int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* value);
+/* Scene::BuildOctree (scene.h:26, scene.cpp:75-83; called by main.cpp:312
+ * with the OBJ bounds +- 0.7 x their size): builds the reference's octree
+ * (scene.cpp:99-160, host) over the scene's triangles and keeps it on the
+ * device.  The BVH answers every query; the octree answers the two kinds of
+ * query where the reference's answer is not the BVH's closest hit: a
+ * closest hit whose t two or more triangles share (the reference keeps the
+ * first in its depth-first visit order, scene.cpp:29-48) and a ray its root
+ * box test rejects (scene.cpp:25).  Without it (or with option tie_rule =
+ * index) ties go to the lowest triangle index and no ray is rejected. */
+int tmpt_scene_build_octree(tmpt_scene* scene, const float bmin[3], const float bmax[3]);
+/* The root box main.cpp:312 gives BuildOctree: sceneMin - extra, sceneMax + extra
+ * with extra = (sceneMax - sceneMin) * 0.7 (main.cpp:294-295); bmin / bmax
+ * are tmpt_load_obj's OBJ bounds.  box = {min.xyz, max.xyz}. */
+int tmpt_octree_bounds(const float bmin[3], const float bmax[3], float box[6]);
+/* Check hook (host only, no device): the octree tmpt_scene_build_octree would
+ * build: out = {nodes, leaves, triangle references, depth, FNV-1a digest of
+ * the preorder walk (box bits, leaf lists)}.  Tests compare it with the
+ * oracle's octree. */
+int tmpt_octree_digest(const float* tris, int32_t n, const float bmin[3], const float bmax[3], uint64_t out[5]);
 /* Scene::~Scene (scene.h:20) */
 int tmpt_scene_destroy(tmpt_scene* scene);
 
-/* Scene::HitScene (scene.h:36-37, scene.cpp:129-140), batched:
+/* Scene::HitScene (scene.h:36-37, scene.cpp:86-97), batched:
  * rays = n x {orig.xyz, dir.xyz} (dir normalised), hits = n x {pos.xyz,
  * normal.xyz, t} written where ids[i] >= 0; ids[i] = index of the closest
  * triangle or -1 (the reference returns 1 instead of the index).  any_hit != 0
@@ -217,10 +263,11 @@ int tmpt_render(tmpt_scene* scene, const tmpt_camera* cam, const tmpt_render_des
  * num_shards are taken over; *seconds = wall time from the renders' start to
  * the assembled frame on devices[0] (scene builds excluded, main.cpp:319-333);
  * *ray_count = all devices' rays.  The one-process-per-GPU form is bench.py
- * (torch.distributed + RCCL). */
-int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, const tmpt_render_desc* desc,
-                      const int32_t* devices, int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count,
-                      double* seconds);
+ * (torch.distributed + RCCL).  octree_box: each device's scene also builds the
+ * reference's octree over it (tmpt_scene_build_octree), as main.cpp:312 does. */
+int tmpt_render_multi(const float* tris, int32_t n, const float* octree_box /* bmin[3], bmax[3] or NULL */,
+                      const tmpt_camera* cam, const tmpt_render_desc* desc, const int32_t* devices,
+                      int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count, double* seconds);
 
 /* rows in the tile of desc's shard; global row of tile row r */
 int32_t tmpt_tile_rows(const tmpt_render_desc* desc);

@@ -73,6 +73,7 @@ _destroy = _sig("orc_scene_destroy", None, [ctypes.c_void_p])
 _hit_batch = _sig("orc_hit_batch", None, [ctypes.c_void_p, _f32p, ctypes.c_int64, ctypes.c_float,
                                           ctypes.c_float, _f32p, _i32p, ctypes.c_int32])
 _stats = _sig("orc_scene_stats", None, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)])
+_oct_digest = _sig("orc_octree_digest", ctypes.c_uint64, [ctypes.c_void_p])
 _render = _sig("orc_render", ctypes.c_uint64, [ctypes.c_void_p, ctypes.POINTER(_Camera), ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -197,7 +198,7 @@ def load_scene(path: str):
 
 
 class Scene:
-    """Oracle scene: accel = ACCEL_OCTREE (the reference's, scene.cpp:118-203),
+    """Oracle scene: accel = ACCEL_OCTREE (the reference's, scene.cpp:75-83, 99-160),
     ACCEL_BVH (exact linear-scan semantics, own BVH) or ACCEL_LINEAR."""
 
     def __init__(self, tris, accel=ACCEL_OCTREE, tie=TIE_VISIT, bmin=None, bmax=None):
@@ -231,6 +232,11 @@ class Scene:
         a = (ctypes.c_int64 * 4)()
         _stats(self._h, a)
         return list(a)
+
+    def octree_digest(self) -> int:
+        """FNV-1a of the octree's preorder walk (0 for other accelerators' scenes
+        it is the empty hash)."""
+        return int(_oct_digest(self._h))
 
     def render(self, cam_arr, w, h, spp, seed_mode=SEED_ROW, y0=0, y1=None, row_step=1,
                threads=None, rgba=None, x0=0, x_step=1):

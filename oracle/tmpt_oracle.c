@@ -273,7 +273,7 @@ static inline int ray_tri(v3 ro, v3 rd, const tri_t* tri, float tMin, float tMax
     return 0;
 }
 
-/* RayHitAabb, maths.h:116-134; r_inv.dir is 1/dir (scene.cpp:135-136) */
+/* RayHitAabb, maths.h:116-134; r_inv.dir is 1/dir (scene.cpp:92-93) */
 static inline int ray_hit_aabb(v3 o, v3 invd, v3 bmin, v3 bmax, float tMin, float tMax)
 {
     for (int c = 0; c < 3; ++c) {
@@ -437,16 +437,16 @@ static void oct_push_tris(orc_scene* s, const int32_t* ids, int32_t cnt, int64_t
     s->n_oct_tris += cnt;
 }
 
-/* OctreeNode::Subdivide / InternalDivide, scene.cpp:142-203.  `ids` is the
+/* OctreeNode::Subdivide / InternalDivide, scene.cpp:99-160.  `ids` is the
  * node's triangle list (indices into the scene copy, in reference order). */
 static void oct_subdivide(orc_scene* s, int64_t node, int32_t* ids, int32_t cnt, int depth)
 {
-    if (!(cnt > 10 && depth < 10)) { /* scene.cpp:144 */
+    if (!(cnt > 10 && depth < 10)) { /* scene.cpp:101 */
         s->oct[node].first_child = -1;
         oct_push_tris(s, ids, cnt, node);
         return;
     }
-    int cdepth = depth + 1; /* InternalDivide(depth + 1), scene.cpp:146 */
+    int cdepth = depth + 1; /* InternalDivide(depth + 1), scene.cpp:103 */
     v3 pmin = s->oct[node].bmin, pmax = s->oct[node].bmax;
     const v3 half = vscale(vsub(pmax, pmin), 0.5f);
     int64_t first = s->n_oct;
@@ -457,7 +457,7 @@ static void oct_subdivide(orc_scene* s, int64_t node, int32_t* ids, int32_t cnt,
     static const float ox[8] = {0, 1, 0, 1, 0, 1, 0, 1};
     static const float oy[8] = {0, 0, 0, 0, 1, 1, 1, 1};
     static const float oz[8] = {0, 0, 1, 1, 0, 0, 1, 1};
-    for (int i = 0; i < 8; ++i) { /* scene.cpp:162-184 */
+    for (int i = 0; i < 8; ++i) { /* scene.cpp:119-141 */
         v3 cmin;
         if (i == 0) cmin = pmin;
         else if (i == 7) cmin = vadd(pmin, half);
@@ -466,7 +466,7 @@ static void oct_subdivide(orc_scene* s, int64_t node, int32_t* ids, int32_t cnt,
         s->oct[first + i].bmax = vadd(cmin, half);
     }
     int32_t* sub = (int32_t*)malloc((size_t)(cnt > 0 ? cnt : 1) * sizeof(int32_t));
-    for (int i = 0; i < 8; ++i) { /* scene.cpp:187-200 */
+    for (int i = 0; i < 8; ++i) { /* scene.cpp:144-157 */
         int64_t c = first + i;
         v3 cmin = s->oct[c].bmin, cmax = s->oct[c].bmax;
         v3 center = vscale(vadd(cmin, cmax), 0.5f);
@@ -630,7 +630,7 @@ orc_scene* orc_scene_create(const float* tris, int32_t n, int32_t accel, int32_t
     s->n = n;
     s->accel = accel;
     s->tie_mode = tie_mode;
-    s->tris = (tri_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(tri_t)); /* scene.cpp:97-100 */
+    s->tris = (tri_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(tri_t)); /* scene.cpp:54-57 */
     for (int32_t i = 0; i < n; ++i) {
         s->tris[i].v0 = vload(tris + 9 * i);
         s->tris[i].v1 = vload(tris + 9 * i + 3);
@@ -638,7 +638,7 @@ orc_scene* orc_scene_create(const float* tris, int32_t n, int32_t accel, int32_t
     }
     int32_t* ids = (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
     for (int32_t i = 0; i < n; ++i) ids[i] = i;
-    if (accel == ORC_ACCEL_OCTREE) { /* BuildOctree, scene.cpp:118-126 */
+    if (accel == ORC_ACCEL_OCTREE) { /* BuildOctree, scene.cpp:75-83 */
         int64_t root = oct_alloc_node(s);
         s->oct[root].bmin = vload(oct_min);
         s->oct[root].bmax = vload(oct_max);
@@ -676,7 +676,39 @@ void orc_scene_stats(const orc_scene* s, int64_t out[4])
     out[3] = s->n;
 }
 
-/* Scene::HitScene, scene.cpp:129-140 (returns the triangle index, not 1) */
+/* FNV-1a over the octree in depth-first preorder (each node's box bits, then
+ * for a leaf its triangle count and list) -- the same walk the library's
+ * tmpt_octree_digest hashes, so the two octrees can be compared node for node. */
+static void fnv_word(uint64_t* h, uint32_t w)
+{
+    for (int b = 0; b < 4; ++b) *h = (*h ^ ((w >> (8 * b)) & 255u)) * 1099511628211ull;
+}
+static void oct_digest_rec(const orc_scene* s, int64_t node, uint64_t* h)
+{
+    const oct_node* nd = &s->oct[node];
+    const float f[6] = {nd->bmin.x, nd->bmin.y, nd->bmin.z, nd->bmax.x, nd->bmax.y, nd->bmax.z};
+    for (int k = 0; k < 6; ++k) {
+        uint32_t u;
+        memcpy(&u, &f[k], 4);
+        fnv_word(h, u);
+    }
+    fnv_word(h, nd->first_child < 0 ? 1u : 0u);
+    if (nd->first_child < 0) {
+        fnv_word(h, (uint32_t)nd->tri_cnt);
+        for (int32_t k = 0; k < nd->tri_cnt; ++k) fnv_word(h, (uint32_t)s->oct_tris[nd->tri_off + k]);
+    } else {
+        for (int i = 0; i < 8; ++i) oct_digest_rec(s, nd->first_child + i, h);
+    }
+}
+
+uint64_t orc_octree_digest(const orc_scene* s)
+{
+    uint64_t h = 1469598103934665603ull;
+    if (s->accel == ORC_ACCEL_OCTREE && s->n_oct > 0) oct_digest_rec(s, 0, &h);
+    return h;
+}
+
+/* Scene::HitScene, scene.cpp:86-97 (returns the triangle index, not 1) */
 static int32_t hit_scene(const orc_scene* s, v3 ro, v3 rd, float tMin, float tMax, hit_t* out)
 {
     int32_t hitId = -1;

@@ -38,7 +38,7 @@ typedef struct orc_scene orc_scene;
 /* scene query accelerators */
 enum { ORC_ACCEL_OCTREE = 0, ORC_ACCEL_BVH = 1, ORC_ACCEL_LINEAR = 2 };
 /* tie handling among equal-t hits:
- *   ORC_TIE_VISIT: first found in visit order wins (strict '<', scene.cpp:77)
+ *   ORC_TIE_VISIT: first found in visit order wins (strict '<', scene.cpp:34)
  *   ORC_TIE_INDEX: lowest triangle index wins (= linear scan with strict '<') */
 enum { ORC_TIE_VISIT = 0, ORC_TIE_INDEX = 1 };
 /* RNG seeding: ROW = main.cpp:204 unmodified; PIXEL = per-pixel seed */
@@ -77,7 +77,7 @@ void orc_free(void* p);
 orc_scene* orc_scene_create(const float* tris, int32_t n, int32_t accel, int32_t tie_mode,
                             const float oct_min[3], const float oct_max[3]);
 void       orc_scene_destroy(orc_scene* s);
-/* HitScene (scene.cpp:129-140) with the triangle index reported (-1 on miss).
+/* HitScene (scene.cpp:86-97) with the triangle index reported (-1 on miss).
  * hit_out = {pos.xyz, normal.xyz, t}; written only on a hit. */
 int32_t    orc_hit_scene(const orc_scene* s, const float orig[3], const float dir[3],
                          float tmin, float tmax, float hit_out[7]);
@@ -86,6 +86,8 @@ void       orc_hit_batch(const orc_scene* s, const float* rays, int64_t n, float
                          float tmax, float* hits, int32_t* ids, int32_t nthreads);
 /* statistics of the octree (node count, leaf count, triangle references) */
 void       orc_scene_stats(const orc_scene* s, int64_t out[4]);
+/* FNV-1a of the octree's preorder walk (box bits, leaf lists): see the C file */
+uint64_t   orc_octree_digest(const orc_scene* s);
 
 /* ---- Tracer (main.cpp:44-119, 172-246) ----
  * Renders rows y = y0, y0+row_step, ... < y1 into rgba (full-frame layout,

@@ -67,3 +67,19 @@ def test_gloo_ranks_render_shards_and_assemble_frame(tmp_path, world):
     assert np.array_equal(frame, full)
     shard_rays, full_rays = np.load(out + ".rays.npy")
     assert shard_rays == full_rays
+
+
+def test_bench_refuses_a_mislabelled_gpu_count():
+    """bench.py never measures another GPU count than --gpus says: under a
+    launcher WORLD_SIZE must equal it, and without one on a machine with too
+    few GPUs for one RCCL rank each it exits non-zero (no GPU here)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 2 and "GPU" in r.stderr and not r.stdout.strip()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1"], cwd=root, capture_output=True, text=True,
+                       timeout=300, env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and "WORLD_SIZE 2" in r.stderr and not r.stdout.strip()

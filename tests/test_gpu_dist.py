@@ -68,3 +68,29 @@ def test_bench_rccl_path_one_rank(gpu, tmp_path):
     a = np.asarray(Image.open(one).convert("RGBA"))
     b = np.asarray(Image.open(rccl).convert("RGBA"))
     assert np.array_equal(a, b)
+
+
+def test_bench_gpus_n_launches_its_own_ranks(gpu, tmp_path):
+    """`python bench.py --gpus 2` with no launcher around it starts its two
+    ranks itself (torch.distributed.run as a child, before any GPU call): with
+    the gloo rehearsal both share the box's GPU and the line says n_gpus 2;
+    with nccl (one rank per GPU) on a box with fewer GPUs it exits non-zero
+    and says why, instead of measuring one GPU."""
+    import toymeshpathtracer_amd as tm
+    two = tmp_path / "two.png"
+    one = tmp_path / "one.png"
+    common = ["--config", "teapot720", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-compare"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r1 = _bench(["bench.py", "--gpus", "1", "--save", str(one)] + common)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--save", str(two)] + common,
+                       cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
+    assert np.array_equal(np.asarray(Image.open(one)), np.asarray(Image.open(two)))
+    if tm.device_count() < 2:
+        r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + common, cwd=ROOT, capture_output=True,
+                           text=True, timeout=300, env=env)
+        assert r.returncode != 0 and "visible GPUs" in r.stderr and not r.stdout.strip()

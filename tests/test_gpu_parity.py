@@ -27,9 +27,17 @@ REFERENCE_BINARY = {
 }
 
 
-def _scene(name, device=0):
+def _scene(name, device=0, octree=False):
+    """octree: build the reference's octree too (main.cpp:312), so the scene
+    answers as the reference does (tied closest hits in its visit order, its
+    root box test); without it ties go to the lowest index."""
     tris, bmin, bmax = tm.load_scene(data(name))
-    return tris, bmin, bmax, tm.Scene(tris, device=device)
+    return tris, bmin, bmax, tm.Scene(tris, device=device, bounds=(bmin, bmax) if octree else None)
+
+
+def _ref_oracle(tris, bmin, bmax):
+    """The reference's own algorithm: octree, first strict '<' in visit order."""
+    return oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
 
 
 def _png_order_sha(img):
@@ -61,23 +69,46 @@ def _random_rays(tris, n, seed):
     return np.concatenate([o, d], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("name", ["triangle.obj", "cube.obj", "suzanne.obj", "teapot.obj"])
-def test_hitscene_kat(gpu, name):
-    """Scene::HitScene on 200k rays: same triangle, same t/pos/normal bits as
-    the oracle's exact-semantics query (= linear scan with strict '<')."""
-    tris, bmin, bmax, sc = _scene(name)
-    rays = _random_rays(tris, 200_000, seed=7)
-    ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
-    oids, ohits = osc.hit_batch(rays, 0.001, 1.0e7)
-    assert (ids >= 0).sum() > 1000
+def _same_answers(ids, hits, oids, ohits):
     mism = np.nonzero(ids != oids)[0]
     assert mism.size == 0, f"{mism.size} id mismatches, first {mism[:5]} gpu {ids[mism[:5]]} oracle {oids[mism[:5]]}"
     h = ids >= 0
     assert np.array_equal(hits[h].view(np.uint32), ohits[h].view(np.uint32))
+
+
+# rays of test_hitscene_kat (seed 7) on which the reference's octree answers
+# differently from the exact closest hit (oracle, counted in this container):
+# (t ties it breaks in visit order, rays its root box test drops)
+KAT_REFERENCE_DEVIATIONS = {"triangle.obj": (0, 296), "cube.obj": (1022, 52), "suzanne.obj": (167, 0),
+                            "teapot.obj": (87, 0)}
+
+
+@pytest.mark.parametrize("name", ["triangle.obj", "cube.obj", "suzanne.obj", "teapot.obj"])
+def test_hitscene_kat(gpu, name):
+    """Scene::HitScene on 200k rays, a third of the aimed ones snapped onto
+    edges and vertices (t ties between triangles sharing them).
+    With the reference's octree built (main.cpp:312): the same triangle and
+    the same t/pos/normal bits as the reference's own algorithm -- octree,
+    first strict '<' in visit order, its root box test (oracle octree) --
+    including every tie and root-box miss where that differs from the exact
+    closest hit.  With option tie_rule=index: the exact-semantics contract
+    (oracle BVH = linear scan with strict '<', lowest index on a tie)."""
+    tris, bmin, bmax, sc = _scene(name, octree=True)
+    rays = _random_rays(tris, 200_000, seed=7)
+    ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
+    st = sc.stats()
+    assert (ids >= 0).sum() > 1000
+    _same_answers(ids, hits, *_ref_oracle(tris, bmin, bmax).hit_batch(rays, 0.001, 1.0e7))
+    ties, roots = KAT_REFERENCE_DEVIATIONS[name]
+    assert st.tie_rule == 0 and st.tie_queries >= ties and (st.root_misses > 0) == (roots > 0)
     # any-hit: same hit/miss bit
     aids, _ = sc.hit_scene_batch(rays, 0.001, 1.0e7, any_hit=True)
     assert np.array_equal(aids >= 0, ids >= 0)
+    sc.set_option("tie_rule", 1)
+    ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
+    assert sc.stats().tie_rule == 1 and sc.stats().tie_queries == 0
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    _same_answers(ids, hits, *osc.hit_batch(rays, 0.001, 1.0e7))
     sc.close()
 
 
@@ -184,7 +215,7 @@ def test_hitscene_nan_and_degenerate_rays(gpu):
 
 
 def test_hitscene_reference_contract(gpu):
-    """Single-ray form returns 1 / -1 like scene.cpp:132-139."""
+    """Single-ray form returns 1 / -1 like scene.cpp:86-97."""
     tris, bmin, bmax, sc = _scene("cube.obj")
     c = (bmin + bmax) / 2
     o = np.array([c[0], c[1], c[2] + 10.0], np.float32)
@@ -202,7 +233,7 @@ def test_row_mode_reproduces_reference_binary(gpu, name, engine):
     reference binary's, byte for byte (SHA-256 recorded in SURVEY.md §8c), and
     the ray count matches.  Megakernel = one lane per row chain; persistent =
     the speculative row engine (render_rowspec)."""
-    tris, bmin, bmax, sc = _scene(name + ".obj")
+    tris, bmin, bmax, sc = _scene(name + ".obj", octree=True)
     cam = tm.Camera.for_scene(bmin, bmax, 640, 360)
     img, rays = sc.trace_image(cam, 640, 360, 4, seed_mode=tm.SEED_ROW, engine=engine)
     sha, krays = REFERENCE_BINARY[name]
@@ -262,8 +293,34 @@ def test_rowstream_fallback_wide_rows(gpu):
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
     b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
-    assert sc.stats().iterations > 1
+    assert sc.stats().iterations > 1 and sc.stats().row_engine == 2 and sc.stats().stream_fallbacks == 0
     assert ra == rb and np.array_equal(a, b)
+    sc.close()
+
+
+def test_rowstream_abort_falls_back_exactly(gpu):
+    """The streaming engine's abort path: with its chasers made to
+    leave at once (test hook rowstream_test_abort) no chain moves, the
+    workers' watchdog aborts the launch, and the frame is rendered again by
+    the iterated engine -- whose image and ray count must be the row chains'
+    exactly, so nothing the aborted launch left in the shared buffers (chain
+    list, colour buffer, counters) leaks into it.  The stats say so; the next
+    render, hook off, streams again."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    w, h, spp = 320, 180, 8
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_MEGAKERNEL)
+    assert sc.stats().row_engine == 1
+    sc.set_option("rowstream_test_abort", 1)
+    b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    st = sc.stats()
+    assert st.stream_fallbacks == 1 and st.row_engine == 2 and st.iterations > 1
+    assert rb == ra and np.array_equal(b, a)
+    sc.set_option("rowstream_test_abort", 0)
+    c, rc = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
+    st = sc.stats()
+    assert st.stream_fallbacks == 0 and st.row_engine == 3 and st.iterations == 1
+    assert rc == ra and np.array_equal(c, a)
     sc.close()
 
 
@@ -291,20 +348,22 @@ def test_rowspec_shards_and_oracle(gpu):
 
 
 def test_rowspec_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
-    """The bench frame at its full 64 spp in row seeding (the reference's own
-    RNG, each row one chain through 1920 x 64 samples): every 64th row equals
-    the oracle's row loop with the exact HitScene contract (lowest index on a
-    t tie).  Against the octree's visit-order ties (bench.py's parity_sample)
-    a tie changes one path's draws and with them the rest of its row's chain,
-    so those rows differ from that pixel on."""
+    """The bench frame at its full 64 spp in row seeding -- the reference's
+    own RNG, each row one chain through 1920 x 64 samples -- with the
+    reference's octree built: every 64th row equals the reference algorithm
+    (oracle octree, visit-order ties) byte for byte.  A tie answered in
+    another order would change one path's draws and with them the rest of its
+    row's chain.  The streaming row engine rendered it (no fallback)."""
     tris, bmin, bmax = tm.load_scene(sponza_path)
     w, h, spp = 1920, 1080, 64
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
-    with tm.Scene(tris) as sc:
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
         img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, engine=tm.ENGINE_PERSISTENT)
-    assert rays == 1762408338
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
-    ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_ROW, row_step=64, threads=16)
+        st = sc.stats()
+    assert st.row_engine == 3 and st.stream_fallbacks == 0 and st.iterations == 1
+    assert st.tie_queries > 0  # ties occurred and took the octree's visit order
+    osc = _ref_oracle(tris, bmin, bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_ROW, row_step=64, threads=16)
     rows = np.arange(0, h, 64)
     diff = np.nonzero((img[rows] != ref[rows]).any(-1))
     assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
@@ -774,14 +833,23 @@ def test_sample_mode_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
     1920x1080) at its full 64 spp in sample seeding, rendered exactly as
     bench.py renders it (1-row bands, the auto block size) -- against the
     oracle's sample-seeded image loop (main.cpp:202-233) on every 64th row,
-    byte for byte, with the exact HitScene contract (lowest index on a tie)."""
+    byte for byte, with the reference's octree built: the reference's own
+    HitScene answers (ties in its visit order), as the oracle octree gives
+    them.  With tie_rule=index the same rows equal the exact-semantics oracle
+    (lowest index on a tie)."""
     tris, bmin, bmax = tm.load_scene(sponza_path)
     w, h, spp = 1920, 1080, 64
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
-    with tm.Scene(tris) as sc:
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
         img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
-    assert rays == 1762389249  # the bench line's rays_per_step
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+        assert sc.stats().tie_queries > 0
+        sc.set_option("tie_rule", 1)
+        img_ix, rays_ix = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
+    rows = np.arange(0, h, 64)
+    osc_ix = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref_ix, _ = osc_ix.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE, row_step=64)
+    assert np.array_equal(img_ix[rows], ref_ix[rows])
+    osc = _ref_oracle(tris, bmin, bmax)
     ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE, row_step=64)
     rows = np.arange(0, h, 64)
     diff = np.nonzero((img[rows] != ref[rows]).any(-1))
@@ -838,10 +906,10 @@ def test_cli_and_render_multi_sample_seeding(gpu, tmp_path):
     img = np.asarray(Image.open(out).convert("RGBA"))[::-1]  # back to row 0 = bottom
     tris, bmin, bmax = tm.load_scene(data("suzanne.obj"))
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    osc = _ref_oracle(tris, bmin, bmax)  # the CLI builds the reference's octree (main.cpp:312)
     ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
     assert np.array_equal(img, ref)
-    multi, rays, _ = tm.render_multi(tris, cam, w, h, spp, [0, 0], seed_mode=tm.SEED_SAMPLE)
+    multi, rays, _ = tm.render_multi(tris, cam, w, h, spp, [0, 0], seed_mode=tm.SEED_SAMPLE, bounds=(bmin, bmax))
     assert rays == ref_rays and np.array_equal(multi, ref)
 
 
@@ -859,3 +927,44 @@ def test_sample_mode_without_colour_buffer(gpu):
     assert ra == rb and np.array_equal(a, b)
     sc.close()
     sc2.close()
+
+
+# ---------------------------------------------------------------- the reference's tie order
+@pytest.mark.parametrize("engine", [tm.ENGINE_PERSISTENT, tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+@pytest.mark.parametrize("seed,oseed", [(tm.SEED_PIXEL, oracle.SEED_PIXEL), (tm.SEED_SAMPLE, oracle.SEED_SAMPLE)])
+def test_octree_rule_every_engine(gpu, engine, seed, oseed):
+    """With the reference's octree built every engine answers closest hits as
+    the reference does (ties re-answered over the octree where they are met:
+    k_path's shading round, k_wf_trace, the megakernel's query; camera rays
+    from a lens that reaches outside the root box take its root test -- the
+    cube's camera sits on the root's face, main.cpp:297 vs :312): the frame
+    equals the oracle octree's (visit-order ties) byte for byte."""
+    tris, bmin, bmax, sc = _scene("cube.obj", octree=True)
+    w, h, spp = 320, 180, 4
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    img, rays = sc.trace_image(cam, w, h, spp, seed_mode=seed, engine=engine)
+    ref, ref_rays = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oseed)
+    assert rays == ref_rays and np.array_equal(img, ref)
+    sc.close()
+
+
+def test_octree_render_multi_and_rebuild(gpu):
+    """tmpt_render_multi with the octree box builds it on every device's scene
+    (the frame equals the oracle octree's); building the octree again on a
+    scene (another box) replaces the first one."""
+    tris, bmin, bmax = tm.load_scene(data("teapot.obj"))
+    w, h, spp = 200, 120, 2
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    ref, ref_rays = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+    img, rays, _ = tm.render_multi(tris, cam, w, h, spp, [0], seed_mode=tm.SEED_SAMPLE, bounds=(bmin, bmax),
+                                   require_rccl=True)
+    assert rays == ref_rays and np.array_equal(img, ref)
+    with tm.Scene(tris) as sc:
+        assert sc.stats().octree_nodes == 0 and sc.stats().tie_rule == 1
+        sc.build_octree(np.array([-50, -50, -50], np.float32), np.array([50, 50, 50], np.float32))
+        sc.build_octree(*tm.octree_bounds(bmin, bmax))
+        st = sc.stats()
+        want = tm.octree_digest(tris, *tm.octree_bounds(bmin, bmax))
+        assert st.octree_nodes == want["nodes"] and st.octree_refs == want["refs"] and st.tie_rule == 0
+        img2, rays2 = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
+    assert rays2 == ref_rays and np.array_equal(img2, ref)

@@ -9,6 +9,7 @@ reference                   here
 ``LoadScene`` main.cpp:122  :func:`load_scene`
 ``Camera`` maths.cpp:40     :class:`Camera` (+ :meth:`Camera.for_scene`, main.cpp:295-307)
 ``Scene`` scene.h:17        :class:`Scene` (LBVH on the GPU)
+``BuildOctree`` scene.h:26  :meth:`Scene.build_octree` (+ :func:`octree_bounds`, main.cpp:312)
 ``Scene::HitScene`` :36     :meth:`Scene.hit_scene` / :meth:`Scene.hit_scene_batch`
 ``TraceImageBody`` :180     :meth:`Scene.trace_image` (parallel_for, main.cpp:329)
 ``stbi_write_png`` :342     :func:`write_png`
@@ -29,7 +30,7 @@ import numpy as np
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
     "SEED_ROW", "SEED_PIXEL", "SEED_SAMPLE", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
-    "tile_rows", "tile_row_to_y", "render_multi",
+    "tile_rows", "tile_row_to_y", "render_multi", "octree_bounds", "octree_digest",
 ]
 
 SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
@@ -96,7 +97,12 @@ class _Stats(ctypes.Structure):
                 ("bvh_depth", ctypes.c_int32), ("n_tris", ctypes.c_int32),
                 ("device", ctypes.c_int32), ("bvh4_nodes", ctypes.c_int32),
                 ("bvh4_depth", ctypes.c_int32), ("leaf_max", ctypes.c_int32),
-                ("builder_iters", ctypes.c_int32)]
+                ("builder_iters", ctypes.c_int32), ("octree_nodes", ctypes.c_int32),
+                ("octree_leaves", ctypes.c_int32), ("octree_refs", ctypes.c_int64),
+                ("octree_build_ms", ctypes.c_double), ("tie_queries", ctypes.c_uint64),
+                ("root_misses", ctypes.c_uint64), ("row_engine", ctypes.c_int32),
+                ("stream_fallbacks", ctypes.c_int32), ("octree_depth", ctypes.c_int32),
+                ("tie_rule", ctypes.c_int32)]
 
 
 def _sig(name, res, args):
@@ -129,8 +135,11 @@ _scene_hit_ranged = _sig("tmpt_scene_hit_ranged", ctypes.c_int, [ctypes.c_void_p
                                                                  ctypes.c_int32, _f32p, _i32p])
 _render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Camera),
                                              ctypes.POINTER(_Desc), ctypes.c_void_p, _u64p])
+_build_octree = _sig("tmpt_scene_build_octree", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p])
+_octree_bounds = _sig("tmpt_octree_bounds", ctypes.c_int, [_f32p, _f32p, _f32p])
+_octree_digest = _sig("tmpt_octree_digest", ctypes.c_int, [_f32p, ctypes.c_int32, _f32p, _f32p, _u64p])
 _render_multi = _sig("tmpt_render_multi", ctypes.c_int,
-                     [_f32p, ctypes.c_int32, ctypes.POINTER(_Camera), ctypes.POINTER(_Desc),
+                     [_f32p, ctypes.c_int32, _f32p, ctypes.POINTER(_Camera), ctypes.POINTER(_Desc),
                       ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.c_void_p, _u64p,
                       ctypes.POINTER(ctypes.c_double)])
 _tile_rows = _sig("tmpt_tile_rows", ctypes.c_int32, [ctypes.POINTER(_Desc)])
@@ -147,7 +156,8 @@ EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_sc
            "tmpt_device_count", "tmpt_scene_create", "tmpt_scene_create_ex", "tmpt_scene_set_option",
            "tmpt_scene_get_option", "tmpt_scene_destroy", "tmpt_scene_hit", "tmpt_scene_hit_ranged",
            "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
-           "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos")
+           "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos",
+           "tmpt_scene_build_octree", "tmpt_octree_bounds", "tmpt_octree_digest")
 
 
 def _check(rc: int, what: str) -> None:
@@ -190,6 +200,27 @@ def load_scene(path: str) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     finally:
         _free(p)
     return tris, bmin, bmax
+
+
+def octree_bounds(bmin, bmax) -> Tuple[np.ndarray, np.ndarray]:
+    """The root box main.cpp:312 gives BuildOctree for a scene whose OBJ bounds
+    are (bmin, bmax): bmin - extra, bmax + extra, extra = 0.7 x the size
+    (main.cpp:294-295), in float32."""
+    lo, hi = np.asarray(bmin, np.float32), np.asarray(bmax, np.float32)
+    box = np.zeros(6, np.float32)
+    _check(_octree_bounds(_fp(lo), _fp(hi), _fp(box)), "octree_bounds")
+    return box[:3].copy(), box[3:].copy()
+
+
+def octree_digest(tris: np.ndarray, box_min, box_max) -> dict:
+    """The octree Scene.build_octree(box_min, box_max) builds, summarised on
+    the host (no GPU): nodes, leaves, triangle references, depth and an FNV-1a
+    digest of its preorder walk -- the check hook tests compare with the oracle."""
+    t = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    lo, hi = np.asarray(box_min, np.float32), np.asarray(box_max, np.float32)
+    out = (ctypes.c_uint64 * 5)()
+    _check(_octree_digest(_fp(t), t.shape[0], _fp(lo), _fp(hi), out), "octree_digest")
+    return dict(zip(("nodes", "leaves", "refs", "depth", "digest"), (int(v) for v in out)))
 
 
 # ----------------------------------------------------------------------------- camera
@@ -274,6 +305,16 @@ class RenderStats:
     bvh4_depth: int
     leaf_max: int
     builder_iters: int
+    octree_nodes: int
+    octree_leaves: int
+    octree_refs: int
+    octree_build_ms: float
+    tie_queries: int
+    root_misses: int
+    row_engine: int
+    stream_fallbacks: int
+    octree_depth: int
+    tie_rule: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,
@@ -318,20 +359,31 @@ def _options_text(options) -> Optional[bytes]:
 
 
 class Scene:
-    """Scene (scene.h:17-43): triangles copied to the GPU, BVH built there
-    (replaces Scene::BuildOctree, scene.cpp:118-126).
+    """Scene (scene.h:17-43): triangles copied to the GPU, BVH built there.
 
     ``options``: build and render options (include/tmpt.h "Scene options"),
     a dict or "key=value,..." string, e.g. ``{"builder": "lbvh", "leaf_max": 4}``;
-    render options can also be changed later with :meth:`set_option`."""
+    render options can also be changed later with :meth:`set_option`.
+    ``bounds``: the OBJ bounds (bmin, bmax) :func:`load_scene` returns; given,
+    the reference's octree is built over them as main.cpp:312 does
+    (:meth:`build_octree`), so tied closest hits get the reference's answer."""
 
-    def __init__(self, triangles: np.ndarray, device: int = 0, options=None):
+    def __init__(self, triangles: np.ndarray, device: int = 0, options=None, bounds=None):
         tris = np.ascontiguousarray(np.asarray(triangles, np.float32).reshape(-1, 9))
         self._h = ctypes.c_void_p()
         self.n = tris.shape[0]
         self.device = device
         _check(_scene_create_ex(_fp(tris), self.n, device, _options_text(options), ctypes.byref(self._h)),
                "Scene")
+        if bounds is not None:
+            self.build_octree(*octree_bounds(*bounds))
+
+    def build_octree(self, box_min, box_max) -> None:
+        """Scene::BuildOctree(min, max) (scene.cpp:75-83): the reference's octree
+        over the scene, kept on the device to answer closest hits tied on t in
+        its visit order and to apply its root box test (include/tmpt.h)."""
+        lo, hi = np.asarray(box_min, np.float32), np.asarray(box_max, np.float32)
+        _check(_build_octree(self._h, _fp(lo), _fp(hi)), "build_octree")
 
     def set_option(self, key: str, value: float) -> None:
         """A render option (include/tmpt.h); applies to the renders after it."""
@@ -359,7 +411,7 @@ class Scene:
     def __exit__(self, *exc):
         self.close()
 
-    # -- Scene::HitScene (scene.cpp:129-140)
+    # -- Scene::HitScene (scene.cpp:86-97)
     def hit_scene_batch(self, rays: np.ndarray, t_min: Optional[float] = None, t_max: Optional[float] = None,
                         any_hit: bool = False) -> Tuple[np.ndarray, np.ndarray]:
         """rays [n,6] (orig, dir) with one [t_min, t_max] for all, or rays [n,8]
@@ -367,6 +419,8 @@ class Scene:
         scene.h:36-37) with t_min = t_max = None
         -> (ids[n] triangle index or -1, hits[n,7] pos/normal/t)."""
         rays = np.asarray(rays, np.float32)
+        if (t_min is None) != (t_max is None):
+            raise ValueError("hit_scene_batch: give both t_min and t_max, or neither (ranged rays [n,8])")
         ranged = t_min is None and t_max is None
         rays = np.ascontiguousarray(rays.reshape(-1, 8 if ranged else 6))
         n = rays.shape[0]
@@ -382,7 +436,7 @@ class Scene:
 
     def hit_scene(self, orig, direction, t_min: float, t_max: float) -> Tuple[int, Optional[Hit]]:
         """Same contract as the reference: returns (-1, None) on a miss and
-        (1, Hit) on a hit (scene.cpp:81 returns 1, not the index)."""
+        (1, Hit) on a hit (scene.cpp:37 sets 1, not the index)."""
         ids, hits = self.hit_scene_batch(np.concatenate([orig, direction])[None], t_min, t_max)
         if ids[0] < 0:
             return -1, None
@@ -452,12 +506,13 @@ class Scene:
 
 def render_multi(tris: np.ndarray, camera: "Camera", width: int, height: int, spp: int, devices,
                  seed_mode: int = SEED_PIXEL, engine: int = ENGINE_PERSISTENT,
-                 require_rccl: bool = False) -> Tuple[np.ndarray, int, float]:
+                 require_rccl: bool = False, bounds=None) -> Tuple[np.ndarray, int, float]:
     """One frame over several devices in this process (tmpt_render_multi: the
     tiles gathered to devices[0] by one RCCL gather): returns (rgba[height,
     width, 4], rays, seconds from the renders' start to the assembled frame).
     A device may repeat (then the gather is device-to-device copies; with
-    require_rccl that is an error instead)."""
+    require_rccl that is an error instead).  ``bounds`` (OBJ bounds): every
+    device's scene builds the reference's octree (main.cpp:312)."""
     t = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     devs = (ctypes.c_int32 * len(devices))(*devices)
     img = np.zeros((height, width, 4), np.uint8)
@@ -465,7 +520,9 @@ def render_multi(tris: np.ndarray, camera: "Camera", width: int, height: int, sp
     secs = ctypes.c_double()
     d = _desc(width, height, spp, seed_mode, 0, 0, 1, engine, FLAG_REQUIRE_RCCL if require_rccl else 0)
     cam = camera._to_c()
-    _check(_render_multi(t.ctypes.data_as(_f32p), t.shape[0], ctypes.byref(cam), ctypes.byref(d), devs,
+    box = None if bounds is None else np.concatenate(octree_bounds(*bounds)).astype(np.float32)
+    _check(_render_multi(t.ctypes.data_as(_f32p), t.shape[0], None if box is None else _fp(box),
+                         ctypes.byref(cam), ctypes.byref(d), devs,
                          len(devices), img.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays),
                          ctypes.byref(secs)), "render_multi")
     return img, int(rays.value), float(secs.value)

@@ -126,6 +126,8 @@ const OptionDef kOptions[] = {
     {"rowspec_chase", false, 0, 1, &Options::rowspec_chase, nullptr, nullptr},
     {"rowspec_stream", false, 0, 1, &Options::rowspec_stream, nullptr, nullptr},
     {"wf_bins", false, 1, 8, &Options::wf_bins, nullptr, nullptr},
+    {"rowstream_test_abort", false, 0, 1, &Options::rowstream_test_abort, nullptr, nullptr},
+    {"tie_rule", false, 0, 1, &Options::tie_rule, nullptr, nullptr},
 };
 
 const OptionDef* find_option(const char* key)
@@ -207,6 +209,7 @@ int options_parse(Options& o, const char* text, bool allow_build)
         val.erase(0, val.find_first_not_of(" \t"));
         if (key == "builder" && (val == "ploc" || val == "lbvh")) val = val == "lbvh" ? "1" : "0";
         if (key == "collapse" && (val == "greedy" || val == "sah")) val = val == "sah" ? "1" : "0";
+        if (key == "tie_rule" && (val == "visit" || val == "index")) val = val == "index" ? "1" : "0";
         char* endp = nullptr;
         const double v = strtod(val.c_str(), &endp);
         if (val.empty() || !endp || *endp != '\0') {
@@ -369,6 +372,7 @@ int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const cha
     int rc = build_lbvh(s, d_tris);
     if (d_tris) (void)hipFree(d_tris);
     if (rc) return fail(rc);
+    s.tris_host.assign(tris, tris + 9 * (size_t)n);  // Scene::Scene's copy (scene.cpp:54-57): the octree's input
     *out = h;
     return 0;
     TMPT_GUARD_END
@@ -383,6 +387,8 @@ int tmpt_scene_destroy(tmpt_scene* h)
     for (auto& st : s.rs_stream)  // the speculative row engine's group streams
         if (st) (void)hipStreamSynchronize(st);
     if (s.nodes4) (void)hipFree(s.nodes4);
+    if (s.oct) (void)hipFree(s.oct);
+    if (s.oct_refs) (void)hipFree(s.oct_refs);
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);
@@ -410,6 +416,77 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.stream) (void)hipStreamDestroy(s.stream);
     delete h;
     return 0;
+}
+
+int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax[3])
+{
+    TMPT_GUARD_BEGIN
+    if (!h || !bmin || !bmax) return bad("tmpt_scene_build_octree: null argument");
+    Scene& s = h->s;
+    if ((int64_t)s.tris_host.size() != 9 * (int64_t)s.n) return bad("tmpt_scene_build_octree: no triangle copy");
+    TMPT_HIP(hipSetDevice(s.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    OctreeHost t;
+    build_octree(s.tris_host.data(), s.n, bmin, bmax, t);
+    if (t.refs.size() >= (size_t)INT32_MAX || t.nodes.size() >= (size_t)INT32_MAX)
+        return bad("tmpt_scene_build_octree: octree too large");
+    OctNode* d_nodes = nullptr;
+    int32_t* d_refs = nullptr;
+    const size_t nb = t.nodes.size() * sizeof(OctNode), rb = std::max<size_t>(1, t.refs.size()) * sizeof(int32_t);
+    if (hipMalloc(&d_nodes, nb) != hipSuccess || hipMalloc(&d_refs, rb) != hipSuccess ||
+        hipMemcpy(d_nodes, t.nodes.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+        (t.refs.size() && hipMemcpy(d_refs, t.refs.data(), t.refs.size() * sizeof(int32_t), hipMemcpyHostToDevice) !=
+                              hipSuccess)) {
+        if (d_nodes) (void)hipFree(d_nodes);
+        if (d_refs) (void)hipFree(d_refs);
+        return (set_error("tmpt_scene_build_octree: out of device memory"), -1);
+    }
+    if (ensure_counters(s)) {
+        (void)hipFree(d_nodes);
+        (void)hipFree(d_refs);
+        return -1;
+    }
+    if (s.stream) (void)hipStreamSynchronize(s.stream);  // a render in flight may still read the old one
+    if (s.oct) (void)hipFree(s.oct);
+    if (s.oct_refs) (void)hipFree(s.oct_refs);
+    s.oct = d_nodes;
+    s.oct_refs = d_refs;
+    s.n_oct = (int32_t)t.nodes.size();
+    s.n_oct_refs = (int64_t)t.refs.size();
+    s.oct_leaves = t.leaves;
+    s.oct_depth = t.depth;
+    for (int c = 0; c < 3; ++c) {
+        s.oct_lo[c] = bmin[c];
+        s.oct_hi[c] = bmax[c];
+    }
+    s.oct_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+    TMPT_GUARD_END
+}
+
+int tmpt_octree_bounds(const float bmin[3], const float bmax[3], float box[6])
+{
+    if (!bmin || !bmax || !box) return bad("tmpt_octree_bounds: null argument");
+    const f3 lo = mk(bmin[0], bmin[1], bmin[2]), hi = mk(bmax[0], bmax[1], bmax[2]);
+    const f3 extra = (hi - lo) * 0.7f;  // main.cpp:294-295
+    const f3 a = lo - extra, b = hi + extra;  // main.cpp:312
+    box[0] = a.x, box[1] = a.y, box[2] = a.z, box[3] = b.x, box[4] = b.y, box[5] = b.z;
+    return 0;
+}
+
+int tmpt_octree_digest(const float* tris, int32_t n, const float bmin[3], const float bmax[3], uint64_t out[5])
+{
+    TMPT_GUARD_BEGIN
+    if (n < 0 || (n > 0 && !tris) || !bmin || !bmax || !out) return bad("tmpt_octree_digest: bad arguments");
+    OctreeHost t;
+    build_octree(tris, n, bmin, bmax, t);
+    out[0] = t.nodes.size();
+    out[1] = (uint64_t)t.leaves;
+    out[2] = t.refs.size() - (uint64_t)t.leaves;  // triangle references (the count words excluded)
+    out[3] = (uint64_t)t.depth;
+    out[4] = octree_digest(t);
+    return 0;
+    TMPT_GUARD_END
 }
 
 int tmpt_scene_set_option(tmpt_scene* h, const char* key, double value)
@@ -459,6 +536,10 @@ int scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, fl
                 hipMemcpy(hits, d_hits, 28 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(ids, d_ids, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
         rc = (set_error("tmpt_scene_hit: kernel or readback failed"), -1);
+    if (!rc) {
+        s.tie_queries = s.counters_host[kTieCounter];
+        s.root_misses = s.counters_host[kTieCounter + 1];
+    }
     cleanup();
     return rc;
 }
@@ -542,9 +623,9 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     TMPT_GUARD_END
 }
 
-int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, const tmpt_render_desc* desc,
-                      const int32_t* devices, int32_t ndevices, uint8_t* rgba_full, uint64_t* ray_count,
-                      double* seconds)
+int tmpt_render_multi(const float* tris, int32_t n, const float* octree_box, const tmpt_camera* cam,
+                      const tmpt_render_desc* desc, const int32_t* devices, int32_t ndevices, uint8_t* rgba_full,
+                      uint64_t* ray_count, double* seconds)
 {
     TMPT_GUARD_BEGIN
     if (!cam || !desc || !devices || ndevices < 1 || !rgba_full || (n > 0 && !tris))
@@ -608,6 +689,8 @@ int tmpt_render_multi(const float* tris, int32_t n, const tmpt_camera* cam, cons
         for (int g = 0; g < nd; ++g)
             th.emplace_back([&, g]() {
                 rcs[(size_t)g] = tmpt_scene_create(tris, n, devices[g], &scenes[(size_t)g]);
+                if (!rcs[(size_t)g] && octree_box)  // main.cpp:312
+                    rcs[(size_t)g] = tmpt_scene_build_octree(scenes[(size_t)g], octree_box, octree_box + 3);
                 if (rcs[(size_t)g]) errs[(size_t)g] = tmpt_last_error();
             });
         for (auto& t : th) t.join();
@@ -730,6 +813,16 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->bvh4_depth = s.depth4;
     o->leaf_max = s.leaf_max;
     o->builder_iters = s.ploc_iters;
+    o->octree_nodes = s.n_oct;
+    o->octree_leaves = s.oct_leaves;
+    o->octree_refs = s.n_oct ? s.n_oct_refs - s.oct_leaves : 0;
+    o->octree_build_ms = s.oct_build_ms;
+    o->tie_queries = s.tie_queries;
+    o->root_misses = s.root_misses;
+    o->row_engine = s.row_engine;
+    o->stream_fallbacks = s.stream_fallbacks;
+    o->octree_depth = s.oct_depth;
+    o->tie_rule = s.oct && s.opt.tie_rule == 0 ? 0 : 1;
     return 0;
 }
 

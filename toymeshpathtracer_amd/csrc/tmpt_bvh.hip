@@ -1,5 +1,5 @@
 // tmpt_bvh.hip -- on-device LBVH build for gfx950, replacing the reference's
-// octree build (Scene::BuildOctree / OctreeNode::Subdivide, scene.cpp:118-203).
+// octree build (Scene::BuildOctree / OctreeNode::Subdivide, scene.cpp:75-83, 99-160).
 //
 // Pipeline (all on the scene's stream; DESIGN.md "LBVH build"):
 //   1. k_tri_prep     per triangle: TriOrig record (v0,v1,v2,normal), padded leaf

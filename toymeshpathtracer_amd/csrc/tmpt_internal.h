@@ -53,6 +53,34 @@ struct alignas(16) TriOrig {
     float4 c;  // v2.z, normal.xyz
 };
 
+// The reference's own octree (Scene::BuildOctree, scene.cpp:75-83, 99-160),
+// kept for the answers the BVH cannot give by itself: which of several
+// triangles that tie on t the reference returns (its first strict '<' in
+// depth-first child order 0..7, scene.cpp:29-48) and the rays its root box
+// test drops.  Nodes in depth-first preorder, 32 B each:
+//   lo = box min.xyz, w = skip (int bits): the node after this subtree
+//   hi = box max.xyz, w = ref  (int bits): -1 for an inner node; a leaf's
+//        triangles are refs[ref + 1 .. ref + refs[ref]] in the reference's order
+// Built on the host (the reference's build is untimed too, main.cpp:312 vs
+// :319) by tmpt_octree.cpp; read by the device only for flagged queries.
+struct alignas(16) OctNode {
+    float4 lo;
+    float4 hi;
+};
+static_assert(sizeof(OctNode) == 32, "octree node: two dwordx4 loads");
+
+struct OctreeHost {
+    std::vector<OctNode> nodes;
+    std::vector<int32_t> refs;
+    int32_t leaves = 0, depth = 0;
+};
+// Subdivide / InternalDivide of scene.cpp:99-160 from the root box [bmin, bmax]
+// (main.cpp:312: the scene bounds +- 0.7 x their size)
+void build_octree(const float* tris9, int32_t n, const float bmin[3], const float bmax[3], OctreeHost& out);
+// FNV-1a over the preorder walk (node boxes' bits, leaf triangle lists): the
+// structure check the CPU tests compare with the oracle's octree
+uint64_t octree_digest(const OctreeHost& t);
+
 // Box culling is conservative (DESIGN.md "Scene query contract"): leaf boxes are
 // inflated by kBoxPadRel * (|coord| + extent) and the far slab distance is
 // stretched by kTfarSlack, so every triangle the reference would accept is
@@ -66,7 +94,8 @@ constexpr float kTfarSlack = 1.00001f;
 constexpr int kStackTotal = 128;
 
 constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
-constexpr int kRenderCounters = 24;   // ray / visit / round counters of one render
+constexpr int kRenderCounters = 32;   // ray / visit / round counters of one render
+constexpr int kTieCounter = 24;       // [24] tied queries re-answered over the octree, [25] root-box misses
 
 // Per-scene options: the library's control plane in place of environment
 // variables (include/tmpt.h documents each key).  Build options are fixed when
@@ -95,7 +124,11 @@ struct Options {
     int rowspec_noshadow = 1; // row seeding: shadow-free speculation + one full re-trace of the chain
     int rowspec_chase = 1;    // row seeding, shadow-free: the chase walks LDS-staged units, one wave per row
     int rowspec_stream = 1;   // row seeding: the streaming row engine (one launch; 0 = iterations)
+    int rowstream_test_abort = 0;  // test hook: the streaming engine's chasers leave at once, so its
+                                   // watchdog aborts the launch and the iterated engine renders the frame
     int wf_bins = 1;          // wavefront engine: extend sub-queues per segment by direction octant (1, 2, 4, 8)
+    int tie_rule = 0;         // closest hits tied on t: 0 = the reference's octree visit order (needs
+                              // tmpt_scene_build_octree), 1 = the lowest triangle index
 };
 int options_parse(Options& o, const char* text, bool allow_build);
 int options_set(Options& o, const char* key, double value, bool allow_build);
@@ -110,6 +143,21 @@ struct Scene {
     int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
     TriPre* tri_pre = nullptr;
     TriOrig* tri_orig = nullptr;
+    std::vector<float> tris_host;  // the triangles as given (Scene::Scene keeps its copy too)
+    // the reference's octree (tmpt_scene_build_octree), and the counter of
+    // closest-hit queries answered through it in the current call
+    OctNode* oct = nullptr;
+    int32_t* oct_refs = nullptr;
+    int32_t n_oct = 0, oct_leaves = 0, oct_depth = 0;
+    int64_t n_oct_refs = 0;
+    double oct_build_ms = 0.0;
+    float oct_lo[3] = {0, 0, 0}, oct_hi[3] = {0, 0, 0};
+    unsigned long long* ties = nullptr;  // [0] re-answered ties, [1] root-box misses
+    uint64_t tie_queries = 0, root_misses = 0;
+    // row seeding: the engine of the last render (0 none, 1 one lane per row,
+    // 2 iterated speculative, 3 streaming) and whether the streaming engine's
+    // launch aborted and was re-rendered by the iterated one
+    int32_t row_engine = 0, stream_fallbacks = 0;
     Options opt;  // build and render options (tmpt_scene_create_ex / tmpt_scene_set_option)
     hipEvent_t wait_ev = nullptr;  // TMPT_FLAG_WAIT_STREAM: reused across renders
     unsigned long long* counters = nullptr;       // a render's ray / visit counters (device)
@@ -176,6 +224,8 @@ const char* last_error();
 
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
+// tmpt_render.hip: the scene's counters, pinned copy and render events (once)
+int ensure_counters(Scene& s);
 // tmpt_render.hip: sample_seed's byte tables for samples [0, spp) (1024 words each)
 void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab);
 // device radix sort of (key, value) pairs (tmpt_bvh.hip); returns 0 if the

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <vector>
 
 #include "tmpt.h"
@@ -46,6 +47,9 @@ struct RenderArgs {
     // row seeding in the megakernel: rows per wave (lanes 0..row_lanes-1 each
     // run one row's chain; the rest of the wave idles)
     int32_t row_lanes;
+    // camera rays take the reference's root box test first (SceneView::oct
+    // set and the lens may lie outside the root box: render() decides)
+    int32_t root_check;
 };
 
 __device__ __forceinline__ int tile_row_to_y(const RenderArgs& a, int lr)
@@ -122,14 +126,19 @@ __device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float
 template <bool COUNT, int BLOCK, int SL, bool TOPC = false>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
-                                         TravCount& cnt)
+                                         TravCount& cnt, bool root_check)
 {
     int depth = 0;
     f3 color = mk(0.0f, 0.0f, 0.0f);
     while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
         ++rays;
         float t, u, v;
-        int id = mega_query<false, COUNT, TOPC>(sv, o, d, t, u, v, st, cnt);
+        int id = -1;
+        if (depth == 0 && root_check && !octree_root_hit(sv, o, d, kMinT, kMaxT)) {
+            if (sv.ties) atomicAdd(&sv.ties[1], 1ull);  // the camera ray misses the reference's root box
+        } else {
+            id = mega_query<false, COUNT, TOPC>(sv, o, d, t, u, v, st, cnt);
+        }
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
@@ -167,7 +176,7 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
         f3 o, d;
         if (a.jt) rng = sample_seed(a.jt, (uint32_t)s, pseed);  // sample seeding
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-        col = col + trace_path<COUNT, BLOCK, SL, TOPC>(sv, o, d, rng, rays, st, lbuf, cnt);
+        col = col + trace_path<COUNT, BLOCK, SL, TOPC>(sv, o, d, rng, rays, st, lbuf, cnt, a.root_check != 0);
     }
     return pack_pixel(col, a.spp_recip);
 }
@@ -220,7 +229,7 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
 }
 
 // ============================================================ batched HitScene
-// Scene::HitScene (scene.cpp:129-140) over a batch: rays n x {o.xyz, d.xyz}
+// Scene::HitScene (scene.cpp:86-97) over a batch: rays n x {o.xyz, d.xyz}
 // with one [tmin, tmax] for all (RANGED = 0), or n x {o.xyz, d.xyz, tmin, tmax}
 // (RANGED = 1, the per-call range of scene.h:36-37).  hits n x {pos, normal, t}
 // where ids >= 0.
@@ -241,7 +250,13 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         f3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
         const float t0 = RANGED ? r[6] : tmin, t1 = RANGED ? r[7] : tmax;
         float t, u, v;
-        const int id = traverse<ANY, false, BLOCK, SL>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
+        int id = -1;
+        // with the reference's octree: its root box test first (scene.cpp:25)
+        if (sv.oct && !octree_root_hit(sv, o, d, t0, t1)) {
+            if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
+        } else {
+            id = traverse<ANY, false, BLOCK, SL>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
+        }
         ids[i] = id;
         if (id >= 0) {
             f3 pos, nrm;
@@ -298,6 +313,7 @@ struct WfState {
     uint32_t seg_cap;
     uint32_t nbins;  // 1, 2, 4 or 8
     int walk_check;  // relaxed head check before a walking wave's atomic (low load, binned queues)
+    int root_check;  // RenderArgs::root_check: camera rays (depth 0) take the root box test
 };
 
 // octant bin of a direction: bit 0 = x < 0, bit 1 = y < 0, bit 2 = z < 0, low bits only
@@ -423,9 +439,12 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                     trav_init(ts, kMaxT);
                     ++traced;
                     steps = 0;
-                    if (sv.n > 0 && !ray_has_nan(o, d)) {
+                    const bool root_miss = !ANY && s.root_check && s.depth[p] == 0 &&
+                                           !octree_root_hit(sv, o, d, kMinT, kMaxT);
+                    if (root_miss && sv.ties) atomicAdd(&sv.ties[1], 1ull);
+                    if (sv.n > 0 && !ray_has_nan(o, d) && !root_miss) {
                         active = true;
-                    } else if (!ANY) {  // provably no hit (NaN ray, empty scene): a counted miss
+                    } else if (!ANY) {  // provably no hit (NaN ray, empty scene, root box): a counted miss
                         s.hid[p] = -1;
                     }
                 }
@@ -463,6 +482,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                 if (ANY) {
                     if (ts.best >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
                 } else {
+                    settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
                     s.hid[p] = ts.best;
                     s.hit[P + p] = ts.bu;
                     s.hit[2 * P + p] = ts.bv;
@@ -625,7 +645,8 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 //     late unit of a pixel kRssT back never overwrites a live one
 //   chainpos[row] = x << 32 | c: the chain's pixel and next sample's offset
 //   list[(row * W + x) * spp + k] = offset of sample k of pixel x on the chain
-//   ctl: [0] rows done, [1] abort, [2] chain progress ticks, [3] error, [4] P
+//   ctl: [0] rows done, [1] abort, [2] chain progress ticks, [3] error, [4] P,
+//        [5..11] statistics, [12] block arrival tickets (the first nchase are chasers)
 constexpr int kRssT = 8;
 constexpr uint32_t kRssM24 = 0xFFFFFFu;
 struct RsStream {
@@ -643,6 +664,8 @@ struct RsStream {
     uint32_t jlimit;        // na * 2^14: offsets with an anchor
     int nrows, nchase, nw;  // rows, chaser blocks, live pixel windows per row
     float spread;
+    uint32_t watchdog;      // 100-MHz ticks without chain progress before the workers abort
+    int test_abort;         // option rowstream_test_abort: chasers leave at once (the abort path's test)
 };
 
 // M^(2j) row_seed of row `row` (j < na * 2^14)
@@ -883,9 +906,19 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     // SAMP 3, 4 (shadow-free speculation): no light terms, no pending next ray
     __shared__ float s_light[SAMP >= 3 ? 1 : kMaxDepth * BLOCK];
     __shared__ float s_next[SAMP >= 3 ? 1 : 6 * BLOCK];
-    if (SAMP == 4 && (int)blockIdx.x < pc.rss.nchase) {  // the streaming row engine's chasers
-        rss_chaser<BLOCK>(a, pc.rss, (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64));
-        return;
+    if (SAMP == 4) {
+        // The chaser role goes by arrival, not by blockIdx: the first nchase
+        // blocks to START take it, so every chaser is resident by construction
+        // and the workers' spin on chain progress cannot wait on a block that
+        // the dispatcher holds back behind them.
+        __shared__ uint32_t s_ticket;
+        if (threadIdx.x == 0) s_ticket = atomicAdd(&pc.rss.ctl[12], 1u);
+        __syncthreads();
+        const uint32_t ticket = s_ticket;
+        if ((int)ticket < pc.rss.nchase) {
+            if (!pc.rss.test_abort) rss_chaser<BLOCK>(a, pc.rss, (int)(ticket * (BLOCK / 64) + threadIdx.x / 64));
+            return;
+        }
     }
     const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
@@ -1160,6 +1193,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 ps_t = stamp();
                 ps_fetch += ps_t - pt_t;
             }
+            {  // closest hits tied on t: the reference's pick (settle_closest; rare, wave-uniform skip)
+                const bool tie = has_pix && !in_query && !cam && !qany && ts.best >= 0 && (ts.best & kTieBit) != 0;
+                if (wany(tie) && tie) settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
+            }
             // ---- finished queries: shade
             bool finish = false, want_off = false;
             f3 color = mk(0.0f, 0.0f, 0.0f);
@@ -1351,6 +1388,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
+                if (a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
+                    in_query = false;  // a camera ray outside the reference's root box: a counted miss
+                    if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
+                }
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
         }
@@ -1383,7 +1424,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (tick != wd_tick || wd_time == 0) {
                     wd_tick = tick;
                     wd_time = now;
-                } else if (now - wd_time > 100000000ull) {
+                } else if (now - wd_time > (uint64_t)pc.rss.watchdog) {
                     if (lane_id() == 0) atomicExch(&pc.rss.ctl[1], 1u);
                     exhausted = true;
                 }
@@ -1905,7 +1946,17 @@ int ensure_ws(Scene& s, size_t bytes)
     return 0;
 }
 
-SceneView view(const Scene& s) { return SceneView{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4}; }
+SceneView view(const Scene& s)
+{
+    SceneView v{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4};
+    if (s.oct && s.opt.tie_rule == 0) {  // the reference's visit order for ties
+        v.oct = s.oct;
+        v.oct_refs = s.oct_refs;
+        v.n_oct = s.n_oct;
+        v.ties = s.ties;
+    }
+    return v;
+}
 
 // Columns of M^n, M the xorshift32 step as a GF(2) 32x32 matrix (maths.cpp:5-13):
 // column j = image of bit j.
@@ -1988,6 +2039,7 @@ RenderArgs make_args(const tmpt_camera* c, const tmpt_render_desc* d)
     a.jt = nullptr;
     a.bmask = 2047u;
     a.row_lanes = 1;  // one row per wave: measured fastest
+    a.root_check = 0;
     return a;
 }
 
@@ -2086,6 +2138,7 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     // low load: under two queue entries per resident traversal lane; binned
     // queues always (most of their sub-queues are empty)
     st.walk_check = nbins > 1 || P < 2 * (int64_t)grid_t * kBlk;
+    st.root_check = a.root_check;
     uint32_t* ovf = w + o_ovf;
     hipStream_t str = s.stream;
 
@@ -2406,8 +2459,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 // blocks chase the rows' chains while the rest trace the windows' units, then
 // the chain's samples in full (k_path<SAMP 2> over the chain list) and the
 // in-order sums (k_resolve_px).  Returns 1 when it does not apply (limits,
-// memory) or the launch aborted (its watchdog: no chain progress for ~1 s),
-// and the caller runs render_rowspec instead.
+// memory) and 2 when the launch aborted (its watchdog: no chain progress for
+// ~1 s); the caller runs render_rowspec instead.
 int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
 {
     const Options& o = s.opt;
@@ -2466,18 +2519,21 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
         have = want;
         return 0;
     };
+    // HBM short after the budget check (another allocation raced it): the
+    // iterated engine may still fit, so fall back rather than fail the frame
+    // (grow() has freed the old buffer; the failed hipMalloc's error is cleared)
     if (grow(s.rss_buf, s.rss_bytes, need) || grow(s.rs_list, s.rs_list_bytes, lneed)) {
-        set_error("render_rowstream: out of device memory");
-        return -1;
+        (void)hipGetLastError();
+        return 1;
     }
     {
         void* sb = s.sbuf;
-        if (grow(sb, s.sbuf_bytes, sneed)) {
-            s.sbuf = nullptr;
-            set_error("render_rowstream: out of device memory");
-            return -1;
-        }
+        const int g = grow(sb, s.sbuf_bytes, sneed);
         s.sbuf = static_cast<float4*>(sb);
+        if (g) {
+            (void)hipGetLastError();
+            return 1;
+        }
     }
     if (!s.rss_tab) {  // M^(2c) and M^(256b) for c, b < 128; M^(2^15 a0), M^(2^20 a1) for a0, a1 < 32
         std::vector<uint32_t> tab, t;
@@ -2530,6 +2586,8 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     S.nrows = rows;
     S.nchase = nchase;
     S.nw = nw;
+    S.watchdog = o.rowstream_test_abort ? 200000u : 100000000u;  // ~1 s (2 ms when testing the abort)
+    S.test_abort = o.rowstream_test_abort;
     // window spread in pixels: 0.055 x room - 0.015, within 0..0.25.  Bench
     // frame, 64 spp (profiles/r03_rowspec/stream_spread_*): best at 0 - 0.02
     // for N = 1 (1.82 s; 2.03 s at the earlier 0.10), 0.06 - 0.08 at 1/2, 0.12 -
@@ -2566,7 +2624,7 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
         fprintf(stderr, "rowstream: aborted (rows done %u of %d, abort %u, error %u); iterated engine instead\n",
                 s.rss_host[0], rows, s.rss_host[1], s.rss_host[3]);
 #endif
-        return 1;
+        return 2;  // launched and aborted: the caller falls back and records it (tmpt_stats.stream_fallbacks)
     }
     // the chain's samples in full (shadows included), then the in-order sums
     k_rss_states<<<(unsigned)((lcap + 255) / 256), 256, 0, s.stream>>>(a, S);
@@ -2923,9 +2981,27 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
 }
 
 // rays: n x 6 floats (one [tmin, tmax] for all) or, ranged, n x 8 (per ray)
+// the render counters (device), their pinned host copy and the render's two
+// timing events: created once per scene, so a render call costs no allocation
+// (it matters for the small shards of a multi-GPU frame); the octree's
+// counters live in the same array (Scene::ties)
+int ensure_counters(Scene& s)
+{
+    if (s.counters) return 0;
+    TMPT_HIP(hipMalloc(&s.counters, kRenderCounters * sizeof(unsigned long long)));
+    TMPT_HIP(hipMemset(s.counters, 0, kRenderCounters * sizeof(unsigned long long)));
+    TMPT_HIP(hipHostMalloc((void**)&s.counters_host, kRenderCounters * sizeof(unsigned long long),
+                           hipHostMallocDefault));
+    for (auto& e : s.render_ev) TMPT_HIP(hipEventCreate(&e));
+    s.ties = s.counters + kTieCounter;
+    return 0;
+}
+
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any, bool ranged,
                     float* d_hits, int32_t* d_ids)
 {
+    if (ensure_counters(s)) return -1;
+    TMPT_HIP(hipMemsetAsync(s.ties, 0, 2 * sizeof(unsigned long long), s.stream));
     auto fn = ranged ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<false, true, kBlk, kSL>)
                      : (any ? k_intersect<true, false, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
@@ -2934,6 +3010,8 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
     if (ensure_ws(s, ovf_bytes)) return -1;
     fn<<<grid, kBlk, 0, s.stream>>>(view(s), d_rays, n, tmin, tmax, d_hits, d_ids, (uint32_t*)s.ws);
     TMPT_HIP(hipGetLastError());
+    TMPT_HIP(hipMemcpyAsync(s.counters_host + kTieCounter, s.ties, 2 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, s.stream));
     return 0;
 }
 
@@ -2996,14 +3074,20 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
             return -1;
         }
     }
-    // the render's counters (device) and their pinned host copy, and the two
-    // timing events: created once per scene, so a render call costs no
-    // allocation (it matters for the small shards of a multi-GPU frame)
-    if (!s.counters) {
-        TMPT_HIP(hipMalloc(&s.counters, kRenderCounters * sizeof(unsigned long long)));
-        TMPT_HIP(hipHostMalloc((void**)&s.counters_host, kRenderCounters * sizeof(unsigned long long),
-                               hipHostMallocDefault));
-        for (auto& e : s.render_ev) TMPT_HIP(hipEventCreate(&e));
+    if (ensure_counters(s)) return -1;
+    // camera rays take the reference's root box test unless the whole lens
+    // (origin +- lens_radius along u and v) lies inside the root box by more
+    // than tMin and a rounding margin: a ray from inside always passes it
+    if (s.oct && s.opt.tie_rule == 0) {
+        const float o[3] = {a.cam.origin.x, a.cam.origin.y, a.cam.origin.z};
+        const float uu[3] = {a.cam.u.x, a.cam.u.y, a.cam.u.z}, vv[3] = {a.cam.v.x, a.cam.v.y, a.cam.v.z};
+        bool inside = true;
+        for (int c = 0; c < 3; ++c) {
+            const double r = (double)a.cam.lens_radius * (std::fabs((double)uu[c]) + std::fabs((double)vv[c]));
+            const double m = 2.0 * kMinT + 1e-4 * ((double)s.oct_hi[c] - (double)s.oct_lo[c]);
+            inside = inside && (double)o[c] - r > (double)s.oct_lo[c] + m && (double)o[c] + r < (double)s.oct_hi[c] - m;
+        }
+        a.root_check = inside ? 0 : 1;
     }
     unsigned long long* d_counters = s.counters;
     TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
@@ -3025,6 +3109,8 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.extend_rays = s.shadow_rays = s.node_visits = s.tri_tests = 0;
     s.shadow_node_visits = s.shadow_tri_tests = 0;
     s.extend_launches = s.shadow_launches = s.iterations = 0;
+    s.row_engine = 0;
+    s.stream_fallbacks = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
@@ -3032,9 +3118,16 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
             // the streaming engine, or the iterated one where it does not apply
             rc = s.opt.rowspec_stream != 0 && s.opt.rowspec_noshadow != 0 ? render_rowstream(s, a, d_out, d_counters)
                                                                           : 1;
-            if (rc == 1) rc = render_rowspec(s, a, d_out, d_counters);
+            s.row_engine = rc == 0 ? 3 : 2;
+            if (rc == 2) {  // the streaming launch aborted: its counters are partial, start over
+                s.stream_fallbacks = 1;
+                TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
+            }
+            if (rc == 1 || rc == 2) rc = render_rowspec(s, a, d_out, d_counters);
+        } else {
+            rc = render_megakernel(s, a, d_out, count, d_counters);
+            if (a.seed_mode == TMPT_SEED_ROW) s.row_engine = 1;
         }
-        else rc = render_megakernel(s, a, d_out, count, d_counters);
     }
     (void)hipEventRecord(e1, s.stream);
     hipError_t se = rc == 0 ? hipMemcpyAsync(s.counters_host, d_counters, kRenderCounters * sizeof(unsigned long long),
@@ -3052,6 +3145,8 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         return -1;
     }
     s.render_ms = ms;
+    s.tie_queries = c[kTieCounter];
+    s.root_misses = c[kTieCounter + 1];
     if (progressive) s.prog_key[6] = a.smp_end < a.spp ? a.smp_end : -1;
     if (persistent) {  // one kernel for both query kinds
         // k_path launches only (the render's other kernels: order keys, sort,

@@ -1,14 +1,18 @@
 // tmpt_traverse.h -- BVH4Q traversal for gfx950: closest hit (Scene::HitScene,
-// scene.cpp:128-140) and any hit (the shadow query of Scatter, main.cpp:57-60,
+// scene.cpp:86-97) and any hit (the shadow query of Scatter, main.cpp:57-60,
 // whose only consumer is the hit/miss bit).  Every engine (persistent path
 // kernel, wavefront, megakernel, batched HitScene) steps the same function,
 // trav_step4q2_mixed.
 //
-// * Scene query contract: result = the reference's closest hit over
-//   all triangles with strict '<', i.e. ties go to the lowest triangle index.
-//   Box culling is conservative (padded leaf boxes, stretched far distance),
-//   so the Moller-Trumbore test alone -- bit-identical to maths.cpp:339-380 --
-//   decides every hit.
+// * Scene query contract: the BVH finds the closest hit over all
+//   triangles.  Box culling is conservative (padded leaf boxes, stretched far
+//   distance), so the Moller-Trumbore test alone -- bit-identical to
+//   maths.cpp:339-380 -- decides every hit.  When two or more triangles share
+//   the closest t, the lowest index is kept and the query is flagged
+//   (kTieBit in TravState::best): the reference keeps the first of them in its
+//   octree's visit order (scene.cpp:29-48), so with the scene's octree built
+//   (tmpt_scene_build_octree) a flagged query is answered again over that
+//   octree, exactly as HitSceneInternal walks it (octree_closest below).
 // * Stack: the first SL entries of each lane live in LDS (layout [depth][lane],
 //   so a wave's accesses to one depth hit 64 distinct banks); deeper entries
 //   spill to a per-lane global area (never more than kStackTotal in all).
@@ -130,7 +134,18 @@ struct SceneView {
     const TriOrig* __restrict__ tri_orig;
     int32_t n;
     int32_t n_nodes4 = 0;
+    // the reference's octree (null: none built, or option tie_rule = index) and
+    // the counters of the queries it answered ([0] ties, [1] root-box misses)
+    const OctNode* __restrict__ oct = nullptr;
+    const int32_t* __restrict__ oct_refs = nullptr;
+    int32_t n_oct = 0;
+    unsigned long long* ties = nullptr;
 };
+
+// TravState::best of a closest-hit query whose t is shared by two or more
+// triangles (the lowest index among them in the low bits)
+constexpr int kTieBit = 1 << 30;
+constexpr int kIdMask = kTieBit - 1;
 
 struct TravCount {
     uint32_t nodes = 0, tris = 0;
@@ -140,7 +155,8 @@ struct TravCount {
 struct TravState {
     int node;   // next node (>=0 internal, <0 leaf = ~slot)
     int sp;     // stack depth
-    int best;   // original triangle index of the current closest hit, -1 if none
+    int best;   // original triangle index of the current closest hit, -1 if none;
+                // | kTieBit when another triangle was accepted at the same t
     float bt, bu, bv;
 };
 
@@ -160,7 +176,8 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
 // slots carry an inverted box and link to the null leaf); the nearest hit
 // child is next, the others are pushed pairwise-ordered.  Leaf: its triangles'
 // Moller-Trumbore tests (bit-exact, maths.cpp:339-380) with t in [tmin, tmax];
-// ties on t go to the lowest triangle index.  `any` (run time): stop at the
+// ties on t keep the lowest triangle index and set kTieBit (the caller settles
+// them, settle_closest).  `any` (run time): stop at the
 // first accepted triangle (the shadow query).  Returns true when the query is
 // finished; ts.node is undefined after that (the next query re-inits it).
 // tlo: lower clamp of a box's entry distance, min(tmin, 0) (boxes behind the
@@ -259,12 +276,15 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
                         t, u, v)) {
                 int id = __float_as_int(c.y);
-                if (t < ts.bt || (t == ts.bt && ts.best >= 0 && id < ts.best)) {
+                const bool tie = t == ts.bt && ts.best >= 0;
+                if (t < ts.bt || (tie && id < (ts.best & kIdMask))) {
                     ts.bt = t;
                     ts.bu = u;
                     ts.bv = v;
-                    ts.best = id;
+                    ts.best = id | (tie ? kTieBit : 0);
                     if (any) return true;
+                } else if (tie) {
+                    ts.best |= kTieBit;
                 }
             }
             return false;
@@ -292,17 +312,18 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                                           mk(b1.z, b1.w, c1.x), tmin, tmax, t1, u1, w1) &&
                              n > 1u;
             const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
-            const bool acc0 = ok0 && (t0 < ts.bt || (t0 == ts.bt && ts.best >= 0 && id0 < ts.best));
+            const bool tie0 = ok0 && t0 == ts.bt && ts.best >= 0;
+            const bool acc0 = ok0 && (t0 < ts.bt || (tie0 && id0 < (ts.best & kIdMask)));
             ts.bt = acc0 ? t0 : ts.bt;
             ts.bu = acc0 ? u0 : ts.bu;
             ts.bv = acc0 ? w0 : ts.bv;
-            ts.best = acc0 ? id0 : ts.best;
-            const bool acc1 = ok1 && !(any && acc0) &&
-                              (t1 < ts.bt || (t1 == ts.bt && ts.best >= 0 && id1 < ts.best));
+            ts.best = (acc0 ? id0 : ts.best) | (tie0 ? kTieBit : 0);
+            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt && ts.best >= 0;
+            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (tie1 && id1 < (ts.best & kIdMask)));
             ts.bt = acc1 ? t1 : ts.bt;
             ts.bu = acc1 ? u1 : ts.bu;
             ts.bv = acc1 ? w1 : ts.bv;
-            ts.best = acc1 ? id1 : ts.best;
+            ts.best = (acc1 ? id1 : ts.best) | (tie1 ? kTieBit : 0);
             if (any && (acc0 || acc1)) return true;
         } else {  // a lone lane (row chains) gains more from the early exits
             if (tri(a0, b0, c0)) return true;
@@ -325,6 +346,102 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
     return false;
 }
 
+// ---------------------------------------------------------------- reference octree
+// RayHitAabb (maths.h:116-134) in the reference's own arithmetic: the slab
+// distances from the inverted direction (scene.cpp:92-93), swapped when it is
+// negative, the range narrowed by its ternaries, rejected once empty.  Exact,
+// not conservative: it decides which leaves the reference visits.
+__device__ __forceinline__ bool ref_slab(f3 o, f3 inv, float4 lo, float4 hi, float tmin, float tmax)
+{
+    const float oc[3] = {o.x, o.y, o.z}, ic[3] = {inv.x, inv.y, inv.z};
+    const float lc[3] = {lo.x, lo.y, lo.z}, hc[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float t0 = (lc[c] - oc[c]) * ic[c], t1 = (hc[c] - oc[c]) * ic[c];
+        if (ic[c] < 0.0f) {
+            const float sw = t0;
+            t0 = t1;
+            t1 = sw;
+        }
+        tmin = t0 > tmin ? t0 : tmin;
+        tmax = t1 < tmax ? t1 : tmax;
+        if (tmax < tmin) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ f3 ref_inverse(f3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+// HitScene's first step, the root box test (scene.cpp:25 on the root): a ray
+// that misses the root misses the scene, whatever the triangles say.  Only a
+// ray from outside the root box can fail it while hitting a triangle (one
+// that grazes the root's faces at the floor's corners, main.cpp:153-162 puts
+// them on the root's boundary).
+__device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax)
+{
+    return ref_slab(o, ref_inverse(d), sv.oct[0].lo, sv.oct[0].hi, tmin, tmax);
+}
+
+// HitSceneInternal (scene.cpp:21-52) over the preorder octree: a node whose
+// box fails the slab test is skipped with its subtree (its skip link); a
+// leaf tests its triangles in list order with the query's range (tMax is
+// never shrunk, scene.cpp:32) and keeps a hit only if t < the best so far
+// (scene.cpp:34), so among equal t the first met in child order 0..7 wins.
+// Returns the triangle index or -1; (t, u, v) of the hit, e1/e2 formed as
+// maths.cpp:341-342 forms them.
+__device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float& bt,
+                                           float& bu, float& bv)
+{
+    const f3 inv = ref_inverse(d);
+    int best = -1;
+    float tb = tmax, ub = 0.0f, vb = 0.0f;
+    for (int i = 0; i < sv.n_oct;) {
+        const float4 lo = sv.oct[i].lo, hi = sv.oct[i].hi;
+        if (!ref_slab(o, inv, lo, hi, tmin, tmax)) {
+            i = __float_as_int(lo.w);
+            continue;
+        }
+        const int ref = __float_as_int(hi.w);
+        if (ref >= 0) {
+            const int cnt = sv.oct_refs[ref];
+            for (int k = 1; k <= cnt; ++k) {
+                const int id = sv.oct_refs[ref + k];
+                const float4* p = reinterpret_cast<const float4*>(sv.tri_orig + id);
+                const float4 a = p[0], b = p[1], c = p[2];
+                const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
+                float t, u, v;
+                if (mt_test(o, d, v0, v1 - v0, v2 - v0, tmin, tmax, t, u, v) && t < tb) {
+                    tb = t;
+                    ub = u;
+                    vb = v;
+                    best = id;
+                }
+            }
+        }
+        ++i;  // a leaf's skip link is the next node; an inner node descends to child 0
+    }
+    bt = tb;
+    bu = ub;
+    bv = vb;
+    return best;
+}
+
+// A finished closest-hit query: a flagged tie is answered again over the
+// octree (the reference's pick among the tied triangles, and its whole answer
+// for that ray); without an octree the lowest index stands.
+__device__ __forceinline__ void settle_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
+                                               TravState& ts)
+{
+    if (ts.best >= 0 && (ts.best & kTieBit)) {
+        if (sv.oct) {
+            if (sv.ties) atomicAdd(&sv.ties[0], 1ull);
+            ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bu, ts.bv);
+        } else {
+            ts.best &= kIdMask;
+        }
+    }
+}
+
 // A ray with a NaN in its origin or direction can never be accepted by
 // Moller-Trumbore (det, u, v and t all become NaN and every comparison of
 // maths.cpp:345-371 is false), so the reference's HitScene returns -1 for it.
@@ -338,7 +455,7 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
            __builtin_isnan(d.y) | __builtin_isnan(d.z);
 }
 
-// Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:129-140).
+// Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:86-97).
 // Returns the original triangle index or -1; (bt, bu, bv) of the hit.  TOPC:
 // the caller's block holds the top BVH levels in LDS (st.top).
 template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false>
@@ -352,6 +469,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
         const float tlo = fminf(tmin, 0.0f);
         while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
+        if (!ANY) settle_closest(sv, r.o, r.d, tmin, tmax, ts);
     }
     bt = ts.bt;
     bu = ts.bu;
