@@ -169,6 +169,10 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  * Build options (only at creation):
  *   builder      ploc (0, default) | lbvh (1): PLOC (Meister & Bittner 2018) or
  *                Karras 2012 LBVH over the same 30-bit Morton order
+ *   layout       aos (0, default) | soa (1): the sample-seeding path kernel and the
+ *                batched HitScene also get the nodes and triangle records as
+ *                planes (56 B / 40 B per node / triangle in 4 / 3 separate
+ *                lines) -- the measured A/B of DESIGN.md section 3
  *   leaf_max     triangles per BVH4 leaf, 1..16 (default 2)
  *   collapse     greedy (0, default) | sah (1): BVH2 -> BVH4 collapse
  *   ploc_radius  PLOC search radius, 1..256 (default 32)
@@ -177,6 +181,8 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   sample_block     sample seeding: samples per work unit, power of two (0 = auto)
  *   sbuf_max         sample seeding: cap in bytes on the per-sample colour
  *                    buffer (0 = 3/4 of free HBM); over the cap a pixel is one unit
+ *   sbuf_pair        sample seeding: a unit's samples 2k and 2k+1 written back to back into
+ *                    one 32-B sector of the colour buffer (1) or each on its own (0)
  *   pilot            pixel seeding: pilot samples of the cost-ordered supply (-1 = auto, 0 = off)
  *   help, pair       pixel seeding: shadow offload to idle lanes (-1 = auto, 0, 1)
  *                    and expensive ranks per 64-rank chunk (-1 = auto, 0..63)

@@ -149,10 +149,11 @@ def test_hitscene_per_ray_ranges(gpu):
 
 @pytest.mark.parametrize("opts", [{"builder": "lbvh"}, {"collapse": "sah"}, {"leaf_max": 4},
                                   {"builder": "lbvh", "leaf_max": 1}, {"ploc_radius": 4, "leaf_max": 16},
-                                  {"collapse": "sah", "sah_c_leaf": 0.2, "sah_c_tri": 2.0}])
+                                  {"collapse": "sah", "sah_c_leaf": 0.2, "sah_c_tri": 2.0}, {"layout": "soa"},
+                                  {"layout": "soa", "leaf_max": 4}])
 def test_build_variants_match_oracle(gpu, opts):
     """Every build option (LBVH builder, SAH collapse and its costs, leaf size,
-    PLOC radius) changes the tree, never the answers: HitScene on 200k rays
+    PLOC radius, the SoA plane layout) changes the tree or its layout, never the answers: HitScene on 200k rays
     and a sample-seeded frame equal the oracle."""
     tris, bmin, bmax = tm.load_scene(data("teapot.obj"))
     sc = tm.Scene(tris, options=opts)

@@ -9,7 +9,8 @@ Variants are separated by ';', options within a variant by '&' (include/tmpt.h
 setting; render options are set on it before each render; ENGINE picks the
 engine.  Every variant's image must equal the first one's (bit-exact contract).
 Harness settings: TUNE_SCENE, TUNE_SHARDS, TUNE_BAND, TUNE_SEED, TUNE_RES,
-TUNE_COUNT; another library build: TMPT_LIB_PATH (one per process)."""
+TUNE_COUNT, TUNE_OCTREE (0: no reference octree, ties by index); another
+library build: TMPT_LIB_PATH (one per process)."""
 import os
 import sys
 import time
@@ -22,7 +23,7 @@ import numpy as np  # noqa: E402
 import toymeshpathtracer_amd as tm  # noqa: E402
 import gen_standin_sponza  # noqa: E402
 
-BUILD_KEYS = ("builder", "leaf_max", "collapse", "ploc_radius", "sah_c_leaf", "sah_c_tri")
+BUILD_KEYS = ("builder", "layout", "leaf_max", "collapse", "ploc_radius", "sah_c_leaf", "sah_c_tri")
 ENGINES = {"wavefront": tm.ENGINE_WAVEFRONT, "persistent": tm.ENGINE_PERSISTENT, "mega": tm.ENGINE_MEGAKERNEL}
 
 variants = sys.argv[1].split(";") if len(sys.argv) > 1 else [""]
@@ -49,9 +50,9 @@ def parse(v):
 scenes = {}
 with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after each variant
     DEFAULTS = {}
-    for _k in ("sample_block", "sbuf_max", "pilot", "help", "pair", "balance", "dprio", "wave_cap", "rowspec",
+    for _k in ("sample_block", "sbuf_max", "sbuf_pair", "pilot", "help", "pair", "balance", "dprio", "wave_cap", "rowspec",
                "rowspec_wmax", "rowspec_windows", "rowspec_spread", "rowspec_groups", "rowspec_noshadow",
-               "rowspec_chase", "rowspec_stream", "wf_bins"):
+               "rowspec_chase", "rowspec_stream", "wf_bins", "tie_rule"):
         try:  # an older library build (TMPT_LIB_PATH) may not know every option
             DEFAULTS[_k] = _probe.get_option(_k)
         except tm.TmptError:
@@ -61,7 +62,8 @@ with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after eac
 def scene_for(env):
     key = tuple((k, env.get(k)) for k in BUILD_KEYS)
     if key not in scenes:
-        sc = tm.Scene(tris, options={k: v for k, v in key if v is not None})
+        sc = tm.Scene(tris, options={k: v for k, v in key if v is not None},
+                      bounds=None if os.environ.get("TUNE_OCTREE") == "0" else (bmin, bmax))
         st = sc.stats()
         print(f"scene {dict(key)}: build {st.build_ms:.1f} ms, bvh4 nodes {st.bvh4_nodes}, depth4 "
               f"{st.bvh4_depth}, ploc iters {st.builder_iters}", flush=True)
@@ -93,8 +95,9 @@ for r in range(rounds):
                 sc.set_option(k, DEFAULTS[k])
         if ref is None:
             ref, ref_rays = img, rays
-        assert np.array_equal(img, ref), f"variant {v!r} changed the image"
-        assert rays == ref_rays, f"variant {v!r} changed the ray count ({rays} vs {ref_rays})"
+        if "tie_rule" not in env:  # the tie rule alone may change answers (include/tmpt.h)
+            assert np.array_equal(img, ref), f"variant {v!r} changed the image"
+            assert rays == ref_rays, f"variant {v!r} changed the ray count ({rays} vs {ref_rays})"
         res[v].append((rays / dt / 1e6, st.extend_ms, st.shadow_ms, dt * 1e3))
 for v, xs in res.items():
     a = np.array(xs)

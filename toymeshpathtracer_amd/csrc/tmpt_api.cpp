@@ -104,6 +104,7 @@ struct OptionDef {
 };
 const OptionDef kOptions[] = {
     {"builder", true, 0, 1, &Options::builder, nullptr, nullptr},
+    {"layout", true, 0, 1, &Options::layout, nullptr, nullptr},
     {"leaf_max", true, 1, kLeafMaxTris, &Options::leaf_max, nullptr, nullptr},
     {"collapse", true, 0, 1, &Options::collapse, nullptr, nullptr},
     {"ploc_radius", true, 1, 256, &Options::ploc_radius, nullptr, nullptr},
@@ -111,6 +112,7 @@ const OptionDef kOptions[] = {
     {"sah_c_tri", true, 0, 1e6, nullptr, &Options::sah_c_tri, nullptr},
     {"sample_block", false, 0, 1024, &Options::sample_block, nullptr, nullptr},
     {"sbuf_max", false, 0, 1e18, nullptr, nullptr, &Options::sbuf_max},
+    {"sbuf_pair", false, 0, 1, &Options::sbuf_pair, nullptr, nullptr},
     {"pilot", false, -1, 512, &Options::pilot, nullptr, nullptr},
     {"help", false, -1, 1, &Options::help, nullptr, nullptr},
     {"pair", false, -1, 63, &Options::pair, nullptr, nullptr},
@@ -210,6 +212,7 @@ int options_parse(Options& o, const char* text, bool allow_build)
         if (key == "builder" && (val == "ploc" || val == "lbvh")) val = val == "lbvh" ? "1" : "0";
         if (key == "collapse" && (val == "greedy" || val == "sah")) val = val == "sah" ? "1" : "0";
         if (key == "tie_rule" && (val == "visit" || val == "index")) val = val == "index" ? "1" : "0";
+        if (key == "layout" && (val == "aos" || val == "soa")) val = val == "soa" ? "1" : "0";
         char* endp = nullptr;
         const double v = strtod(val.c_str(), &endp);
         if (val.empty() || !endp || *endp != '\0') {
@@ -389,6 +392,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.oct) (void)hipFree(s.oct);
     if (s.oct_refs) (void)hipFree(s.oct_refs);
+    if (s.soa_buf) (void)hipFree(s.soa_buf);
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);

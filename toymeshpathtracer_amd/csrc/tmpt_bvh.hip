@@ -672,7 +672,56 @@ __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tr
 
 inline int blocks_for(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
+// layout=soa: the AoS records split into planes (tmpt_internal.h SoaScene)
+__global__ void __launch_bounds__(kBlock) k_soa_planes(const Bvh4Node* __restrict__ nodes, int32_t n4,
+                                                       const TriPre* __restrict__ pre, int32_t n1, uint4* na,
+                                                       uint4* nb, uint2* nc, int4* nd, float4* ta, float4* tb,
+                                                       float2* tc)
+{
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < n4) {
+        const Bvh4Node v = nodes[k];
+        na[k] = make_uint4(__float_as_uint(v.a.x), __float_as_uint(v.a.y), __float_as_uint(v.a.z),
+                           __float_as_uint(v.a.w));
+        nb[k] = v.b;
+        nc[k] = make_uint2(v.c.x, v.c.y);
+        nd[k] = v.d;
+    }
+    if (k < n1) {
+        const TriPre t = pre[k];
+        ta[k] = t.a;
+        tb[k] = t.b;
+        tc[k] = make_float2(t.c.x, t.c.y);
+    }
+}
+
 }  // namespace
+
+int build_soa(Scene& s)
+{
+    const size_t n4 = (size_t)std::max(s.n_nodes4, 1), n1 = (size_t)s.n + 1;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_nb = al(16 * n4), o_nc = o_nb + al(16 * n4), o_nd = o_nc + al(8 * n4), o_ta = o_nd + al(16 * n4),
+                 o_tb = o_ta + al(16 * n1), o_tc = o_tb + al(16 * n1), total = o_tc + al(8 * n1);
+    if (s.soa_buf) (void)hipFree(s.soa_buf);
+    s.soa_buf = nullptr;
+    s.soa = SoaScene();
+    TMPT_HIP(hipMalloc(&s.soa_buf, total));
+    char* b = static_cast<char*>(s.soa_buf);
+    uint4* na = reinterpret_cast<uint4*>(b);
+    uint4* nb = reinterpret_cast<uint4*>(b + o_nb);
+    uint2* nc = reinterpret_cast<uint2*>(b + o_nc);
+    int4* nd = reinterpret_cast<int4*>(b + o_nd);
+    float4* ta = reinterpret_cast<float4*>(b + o_ta);
+    float4* tb = reinterpret_cast<float4*>(b + o_tb);
+    float2* tc = reinterpret_cast<float2*>(b + o_tc);
+    k_soa_planes<<<blocks_for((int64_t)std::max(n4, n1), kBlock), kBlock, 0, s.stream>>>(
+        s.nodes4, s.n_nodes4, s.tri_pre, (int32_t)n1, na, nb, nc, nd, ta, tb, tc);
+    TMPT_HIP(hipGetLastError());
+    TMPT_HIP(hipStreamSynchronize(s.stream));
+    s.soa = SoaScene{na, nb, nc, nd, ta, tb, tc};
+    return 0;
+}
 
 // LSD radix sort of (key, value) pairs by the low `bits` bits of the key
 // (stable; 8 bits per pass, ping-pong).  hist: 256 * ceil(n / kSortTile)
@@ -923,6 +972,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
         return -1;
     }
     if (rc) return rc;
+    if (s.opt.layout == 1 && build_soa(s)) return -1;
     s.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }

@@ -81,6 +81,22 @@ void build_octree(const float* tris9, int32_t n, const float bmin[3], const floa
 // structure check the CPU tests compare with the oracle's octree
 uint64_t octree_digest(const OctreeHost& t);
 
+// Build option layout=soa (the north star's "SoA" A/B):
+// the BVH4Q nodes and the leaf-ordered triangle records as planes, each plane
+// one load of a step -- node planes a (origin, exponents), b (x / y byte
+// planes), c (z byte planes, 8 B: no padding), d (child links); triangle
+// planes a (v0, e1.x), b (e1.yz, e2.xy), c (e2.z, index: 8 B).  56 B per node
+// and 40 B per triangle instead of 64 and 48, in 4 and 3 separate lines.
+struct SoaScene {
+    const uint4* __restrict__ na = nullptr;
+    const uint4* __restrict__ nb = nullptr;
+    const uint2* __restrict__ nc = nullptr;
+    const int4* __restrict__ nd = nullptr;
+    const float4* __restrict__ ta = nullptr;
+    const float4* __restrict__ tb = nullptr;
+    const float2* __restrict__ tc = nullptr;
+};
+
 // Box culling is conservative (DESIGN.md "Scene query contract"): leaf boxes are
 // inflated by kBoxPadRel * (|coord| + extent) and the far slab distance is
 // stretched by kTfarSlack, so every triangle the reference would accept is
@@ -103,6 +119,7 @@ constexpr int kTieCounter = 24;       // [24] tied queries re-answered over the 
 struct Options {
     // build (tmpt_scene_create_ex)
     int builder = 0;      // 0 = PLOC (Meister & Bittner 2018), 1 = LBVH (Karras 2012)
+    int layout = 0;       // 0 = AoS records (64-B nodes, 48-B triangles), 1 = also SoA planes (SoaScene)
     int leaf_max = 2;     // triangles per BVH4 leaf, 1..kLeafMaxTris
     int collapse = 0;     // BVH2 -> BVH4: 0 = greedy largest-area opening, 1 = SAH-optimal
     int ploc_radius = 32; // PLOC nearest-neighbour search radius
@@ -110,6 +127,7 @@ struct Options {
     // render (tmpt_scene_set_option)
     int sample_block = 0;     // sample seeding: samples per work unit, a power of two (0 = auto)
     double sbuf_max = 0.0;    // sample seeding: cap on the per-sample colour buffer, bytes (0 = 3/4 of free HBM)
+    int sbuf_pair = 1;        // sample seeding: a unit's sample pairs written back to back into one 32-B sector
     int pilot = -1;           // pixel seeding: pilot-pass samples of the cost ordering (-1 auto, 0 off)
     int help = -1;            // pixel seeding: shadow offload to idle lanes (-1 auto, 0 off, 1 on)
     int pair = -1;            // pixel seeding: expensive ranks per 64-rank chunk with offload (-1 auto)
@@ -143,6 +161,8 @@ struct Scene {
     int32_t n_nodes4 = 0, depth4 = 0, leaf_max = 0, ploc_iters = 0;
     TriPre* tri_pre = nullptr;
     TriOrig* tri_orig = nullptr;
+    void* soa_buf = nullptr;  // layout=soa: the planes of SoaScene, one allocation
+    SoaScene soa;
     std::vector<float> tris_host;  // the triangles as given (Scene::Scene keeps its copy too)
     // the reference's octree (tmpt_scene_build_octree), and the counter of
     // closest-hit queries answered through it in the current call
@@ -224,6 +244,7 @@ const char* last_error();
 
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
+int build_soa(Scene& s);  // layout=soa planes from the built AoS records
 // tmpt_render.hip: the scene's counters, pinned copy and render events (once)
 int ensure_counters(Scene& s);
 // tmpt_render.hip: sample_seed's byte tables for samples [0, spp) (1024 words each)

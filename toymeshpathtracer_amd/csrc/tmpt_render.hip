@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
 // with one [tmin, tmax] for all (RANGED = 0), or n x {o.xyz, d.xyz, tmin, tmax}
 // (RANGED = 1, the per-call range of scene.h:36-37).  hits n x {pos, normal, t}
 // where ids >= 0.
-template <bool ANY, bool RANGED, int BLOCK, int SL>
+template <bool ANY, bool RANGED, int BLOCK, int SL, bool SOA = false>
 __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* __restrict__ rays,
                                                      int64_t n, float tmin, float tmax,
                                                      float* __restrict__ hits,
@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         if (sv.oct && !octree_root_hit(sv, o, d, t0, t1)) {
             if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
         } else {
-            id = traverse<ANY, false, BLOCK, SL>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
+            id = traverse<ANY, false, BLOCK, SL, false, SOA>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
         }
         ids[i] = id;
         if (id >= 0) {
@@ -710,6 +710,7 @@ struct PathCtl {
     uint32_t nblk, blk;
     float4* __restrict__ sbuf;
     uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp ([pixel][sample]: 1, spp)
+    uint32_t pair;          // sample pairs (2k, 2k+1) of a unit written back to back (one 32-B sector)
     // Speculative row seeding (SAMP 2, render_rowspec): unit u traces ONE
     // sample of tile pixel upix[u] from RNG state ustate[u] and writes its
     // colour with w = draws | rays << 27 to rs_out[u], and its final RNG state
@@ -896,7 +897,7 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
 
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int OCC = 1, int TAIL = 0, int PROF = 0,
-          int HELP = 0, int SAMP = 0>
+          int HELP = 0, int SAMP = 0, bool SOA = false>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -1329,9 +1330,17 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         pc.rs_end[cur_unit] = rng;
                     } else if (SAMP && pc.sbuf) {  // sample seeding, blocks: k_resolve_px sums in sample order
                         typedef float f32x4 __attribute__((ext_vector_type(4)));
-                        __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f},
-                                                    reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss +
-                                                                                        (size_t)pix * pc.sb_sp)));
+                        f32x4* dst = reinterpret_cast<f32x4*>(pc.sbuf + ((size_t)smp * pc.sb_ss + (size_t)pix * pc.sb_sp));
+                        // paired stores (pc.pair): an even sample with a successor in
+                        // the unit is held in `col` (unused with a colour buffer) and
+                        // written with it, back to back into one 32-B sector
+                        const bool odd = (smp & 1u) != 0u;
+                        if (pc.pair && !odd && smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u) {
+                            col = color;
+                        } else {
+                            if (pc.pair && odd) __builtin_nontemporal_store((f32x4){col.x, col.y, col.z, 0.0f}, dst - 1);
+                            __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f}, dst);
+                        }
                     } else
                         col = col + color;
                     ++smp;
@@ -1456,15 +1465,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const bool stepping = in_query && ((ts.node < 0) == leaf_round);
                 bool done = false;
                 if (leaf_round) {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2, SOA>(sv, r, qany, ts, st, cnt);
                 } else {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1, SOA>(sv, r, qany, ts, st, cnt);
                 }
                 if (done) in_query = false;
                 if (stepping && ((kFull && pc.cost_out) || dp0 > 0.0f)) ++psteps;
             } else if (in_query && (ts.node < 0) == leaf_round) {
                 TravCount c1;
-                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true>(sv, r, qany, ts, st, c1)) in_query = false;
+                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true, 0, SOA>(sv, r, qany, ts, st, c1)) in_query = false;
                 TravCount& dst = qany ? cnt_s : cnt;
                 dst.nodes += c1.nodes;
                 dst.tris += c1.tris;
@@ -1949,6 +1958,7 @@ int ensure_ws(Scene& s, size_t bytes)
 SceneView view(const Scene& s)
 {
     SceneView v{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4};
+    v.soa = s.soa;
     if (s.oct && s.opt.tie_rule == 0) {  // the reference's visit order for ties
         v.oct = s.oct;
         v.oct_refs = s.oct_refs;
@@ -2240,8 +2250,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
     // kernel keeps its register allocation)
-    PathFn fn = a.jt ? (count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>
-                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>)
+    // layout=soa: the sample kernel reads the SoA planes (the A/B of DESIGN.md
+    // section 3; the other engines keep the AoS records)
+    const bool soa = s.soa.na != nullptr;
+    PathFn fn = a.jt ? (count ? (soa ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, true>
+                                     : k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>)
+                              : (soa ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, true>
+                                     : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>))
                      : (count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>
                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     const PathFn fn_default = fn;
@@ -2359,6 +2374,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // fetches per 1080p frame); k_resolve_px reads it through LDS
     pc.sb_ss = 1u;
     pc.sb_sp = (uint32_t)a.spp;
+    // A unit of >= 2 samples holds each even sample's colour until the next one
+    // and writes both into the same 32-B sector (spp even: sectors align), so
+    // the two 16-B halves can leave L2 as one write instead of two (option sbuf_pair)
+    pc.pair = pc.sbuf && blk >= 2u && a.spp % 2 == 0 && o.sbuf_pair ? 1u : 0u;
     // Small shards (at most a quarter as many pixels as resident lanes): a wave
     // holds at most 32 pixels at once, so the pixels spread over more SIMD
     // slots and each wave's chain -- the frame's critical path at that load --
@@ -3002,8 +3021,11 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
 {
     if (ensure_counters(s)) return -1;
     TMPT_HIP(hipMemsetAsync(s.ties, 0, 2 * sizeof(unsigned long long), s.stream));
-    auto fn = ranged ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<false, true, kBlk, kSL>)
-                     : (any ? k_intersect<true, false, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>);
+    const bool soa = s.soa.na != nullptr;
+    auto fn = soa ? (ranged ? (any ? k_intersect<true, true, kBlk, kSL, true> : k_intersect<false, true, kBlk, kSL, true>)
+                            : (any ? k_intersect<true, false, kBlk, kSL, true> : k_intersect<false, false, kBlk, kSL, true>))
+                  : (ranged ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<false, true, kBlk, kSL>)
+                            : (any ? k_intersect<true, false, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>));
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (n + kBlk - 1) / kBlk));
     size_t ovf_bytes = (size_t)grid * kBlk * (kStackTotal - kSL) * sizeof(uint32_t);

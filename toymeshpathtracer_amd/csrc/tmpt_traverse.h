@@ -140,6 +140,9 @@ struct SceneView {
     const int32_t* __restrict__ oct_refs = nullptr;
     int32_t n_oct = 0;
     unsigned long long* ties = nullptr;
+    // build option layout=soa (tmpt_internal.h SoaScene): the same nodes and
+    // triangle records as planes, read by the SOA instantiations
+    SoaScene soa;
 };
 
 // TravState::best of a closest-hit query whose t is shared by two or more
@@ -186,7 +189,7 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
 // KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a voted
 // round), so the other kind's code is not emitted.  TOPC: node indices below
 // st.ntop are read from the block's LDS copy of the top levels.
-template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0>
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0, bool SOA = false>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt, float tlo = 0.0f, float tmin = kMinT,
@@ -198,7 +201,12 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         // 32-bit byte offset off an SGPR base: one VALU for the address
         uint4 A, B, C;
         int4 L;
-        if (!TOPC || (uint32_t)ts.node >= st.ntop) {
+        if (SOA && (!TOPC || (uint32_t)ts.node >= st.ntop)) {  // four planes: 16 + 16 + 8 + 16 B
+            const uint32_t k = (uint32_t)ts.node;
+            A = sv.soa.na[k], B = sv.soa.nb[k], L = sv.soa.nd[k];
+            const uint2 c2 = sv.soa.nc[k];
+            C = make_uint4(c2.x, c2.y, 0u, 0u);
+        } else if (!TOPC || (uint32_t)ts.node >= st.ntop) {
             const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
                                                             ((uint32_t)ts.node << 6));
             A = p[0], B = p[1], C = p[2];
@@ -296,8 +304,18 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         const float4* p0 = reinterpret_cast<const float4*>(base + first * (uint32_t)sizeof(TriPre));
         const float4* p1 = reinterpret_cast<const float4*>(base + (first + (n > 1u ? 1u : 0u)) *
                                                                        (uint32_t)sizeof(TriPre));
-        float4 a0 = p0[0], b0 = p0[1], c0 = p0[2];
-        float4 a1 = p1[0], b1 = p1[1], c1 = p1[2];
+        float4 a0, b0, c0, a1, b1, c1;
+        if (SOA) {  // three planes: 16 + 16 + 8 B per triangle
+            const uint32_t f1 = first + (n > 1u ? 1u : 0u);
+            a0 = sv.soa.ta[first], b0 = sv.soa.tb[first];
+            a1 = sv.soa.ta[f1], b1 = sv.soa.tb[f1];
+            const float2 q0 = sv.soa.tc[first], q1 = sv.soa.tc[f1];
+            c0 = make_float4(q0.x, q0.y, 0.0f, 0.0f);
+            c1 = make_float4(q1.x, q1.y, 0.0f, 0.0f);
+        } else {
+            a0 = p0[0], b0 = p0[1], c0 = p0[2];
+            a1 = p1[0], b1 = p1[1], c1 = p1[2];
+        }
         materialize(a0, b0, c0);
         materialize(a1, b1, c1);
         if (KIND == 2) {
@@ -330,8 +348,13 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             if (n > 1u && tri(a1, b1, c1)) return true;
         }
         for (uint32_t k = 2; k < n; ++k) {
-            const float4* p = reinterpret_cast<const float4*>(base + (first + k) * (uint32_t)sizeof(TriPre));
-            if (tri(p[0], p[1], p[2])) return true;
+            if (SOA) {
+                const float2 q = sv.soa.tc[first + k];
+                if (tri(sv.soa.ta[first + k], sv.soa.tb[first + k], make_float4(q.x, q.y, 0.0f, 0.0f))) return true;
+            } else {
+                const float4* p = reinterpret_cast<const float4*>(base + (first + k) * (uint32_t)sizeof(TriPre));
+                if (tri(p[0], p[1], p[2])) return true;
+            }
         }
         if (KIND == 2 && ts.sp <= SL) {  // branch-free pop from the LDS part
             const uint32_t top = st.lds[(uint32_t)max(ts.sp - 1, 0) * BLOCK];
@@ -458,7 +481,7 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
 // Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:86-97).
 // Returns the original triangle index or -1; (bt, bu, bv) of the hit.  TOPC:
 // the caller's block holds the top BVH levels in LDS (st.top).
-template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false>
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false, bool SOA = false>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
                                         float tmax, float& bt, float& bu, float& bv,
                                         TravStack<BLOCK, SL>& st, TravCount& cnt)
@@ -467,7 +490,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
     trav_init(ts, tmax);
     if (sv.n > 0 && !ray_has_nan(r.o, r.d)) {
         const float tlo = fminf(tmin, 0.0f);
-        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
+        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
         if (!ANY) settle_closest(sv, r.o, r.d, tmin, tmax, ts);
     }
