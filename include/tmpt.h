@@ -130,6 +130,7 @@ typedef struct {
                                  frame was rendered again by the iterated engine */
     int32_t octree_depth;
     int32_t tie_rule;         /* in effect: 0 octree visit order, 1 lowest index (no octree / option) */
+    int64_t chain_pixels;     /* pixel seeding: pixels the last render ran as speculative chains */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */
@@ -189,6 +190,9 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   balance, dprio   pixel seeding: SIMD-balanced first chunks (1), longest-
  *                    remaining-first wave priority with offload (1)
  *   wave_cap         pixel seeding: pixels a wave holds at once (0 = auto, 1..64)
+ *   pixel_chains     pixel seeding, cost-ordered: the heaviest pixels per 1024 that run as
+ *                    speculative chains (every even RNG offset past the pilot traced,
+ *                    the chain walked through them) instead of in pass 2 (-1 = auto, 0 = off)
  *   rowspec          row seeding on the persistent engine: 1 = speculative row
  *                    engine, 0 = one lane per row chain
  *   rowspec_wmax, rowspec_windows, rowspec_spread, rowspec_groups,

@@ -969,3 +969,26 @@ def test_octree_render_multi_and_rebuild(gpu):
         assert st.octree_nodes == want["nodes"] and st.octree_refs == want["refs"] and st.tie_rule == 0
         img2, rays2 = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
     assert rays2 == ref_rays and np.array_equal(img2, ref)
+
+
+@pytest.mark.parametrize("per1024", [0, 16, 200, 1024])
+def test_pixel_chains_match_oracle(gpu, per1024):
+    """Pixel seeding with the heaviest pixels run as speculative chains
+    (option pixel_chains: that many per 1024 of the cost order, up to all of
+    them): every even RNG offset past a pixel's pilot state traced
+    shadow-free, the chain walked through them, its samples traced again in
+    full and summed after the pilot's sum -- the frame and the ray count equal
+    the pixel-seeded oracle's, whole and as shard 1 of 3."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    w, h, spp = 320, 180, 8
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    sc.set_option("pixel_chains", per1024)
+    img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    n = sc.stats().chain_pixels
+    assert n == (0 if per1024 == 0 else min(w * h, (w * h * per1024 + 1023) // 1024))
+    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL)
+    assert rays == ref_rays and np.array_equal(img, ref)
+    tile, trays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=1, num_shards=3)
+    assert np.array_equal(tile, ref[1::3])
+    sc.close()

@@ -119,6 +119,7 @@ const OptionDef kOptions[] = {
     {"balance", false, 0, 1, &Options::balance, nullptr, nullptr},
     {"dprio", false, 0, 1, &Options::dprio, nullptr, nullptr},
     {"wave_cap", false, 0, 64, &Options::wave_cap, nullptr, nullptr},
+    {"pixel_chains", false, -1, 1024, &Options::pixel_chains, nullptr, nullptr},
     {"rowspec", false, 0, 1, &Options::rowspec, nullptr, nullptr},
     {"rowspec_wmax", false, 0, 16384, &Options::rowspec_wmax, nullptr, nullptr},
     {"rowspec_windows", false, 0, 32, &Options::rowspec_windows, nullptr, nullptr},
@@ -827,6 +828,7 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->stream_fallbacks = s.stream_fallbacks;
     o->octree_depth = s.oct_depth;
     o->tie_rule = s.oct && s.opt.tie_rule == 0 ? 0 : 1;
+    o->chain_pixels = s.chain_pixels;
     return 0;
 }
 

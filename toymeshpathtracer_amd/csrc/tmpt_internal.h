@@ -134,6 +134,7 @@ struct Options {
     int balance = 1;          // pixel seeding: SIMD-balanced first chunks
     int dprio = 1;            // pixel seeding: longest-remaining-first wave priority with offload
     int wave_cap = 0;         // pixel seeding: pixels a wave holds at once (0 auto, else 1..64)
+    int pixel_chains = -1;    // pixel seeding, ordered: heaviest pixels per 1024 run as speculative chains (-1 auto)
     int rowspec = 1;          // row seeding: speculative row engine (0 = one lane per row chain)
     int rowspec_wmax = 0;     // row seeding: units per window (0 = auto: 24 x spp)
     int rowspec_windows = 0;  // row seeding: windows per row and iteration (0 = auto)
@@ -178,6 +179,7 @@ struct Scene {
     // 2 iterated speculative, 3 streaming) and whether the streaming engine's
     // launch aborted and was re-rendered by the iterated one
     int32_t row_engine = 0, stream_fallbacks = 0;
+    int64_t chain_pixels = 0;  // pixel seeding: pixels of the last render run as speculative chains
     Options opt;  // build and render options (tmpt_scene_create_ex / tmpt_scene_set_option)
     hipEvent_t wait_ev = nullptr;  // TMPT_FLAG_WAIT_STREAM: reused across renders
     unsigned long long* counters = nullptr;       // a render's ray / visit counters (device)

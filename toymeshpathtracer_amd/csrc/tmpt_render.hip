@@ -1630,6 +1630,13 @@ struct RowSpec {
     uint32_t *lpix, *lstate, *lslot, *lcount;
     uint2* scratch;
     uint32_t scap;
+    // Chains: a row is a chain of cw = W pixels x cspp = spp samples from the
+    // row seed.  Pixel chains (pixel seeding, render_pixel_chains): chain r is
+    // tile pixel cpix[r] alone (cw = 1), its samples smp0 .. smp0 + cspp - 1,
+    // from the RNG state the pilot pass left in cinit[pixel].w.
+    const uint32_t* cpix;
+    const float4* cinit;
+    int cw, cspp, smp0;
 };
 
 // Decode of a unit's rs_out.w: draws | rays << 23 | extend rays << 28.
@@ -1639,7 +1646,8 @@ __global__ void __launch_bounds__(256) k_rs_init(RenderArgs a, RowSpec rs)
 {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= rs.nrows) return;
-    rs.rng[r] = row_seed((uint32_t)tile_row_to_y(a, rs.row0 + r));  // main.cpp:204, unmodified
+    rs.rng[r] = rs.cpix ? __float_as_uint(rs.cinit[rs.cpix[r]].w)           // pixel chain: after its pilot
+                        : row_seed((uint32_t)tile_row_to_y(a, rs.row0 + r));  // main.cpp:204, unmodified
     rs.x[r] = rs.k[r] = rs.pdraws[r] = rs.rays[r] = rs.erays[r] = rs.short_win[r] = 0u;
     rs.prev_mean[r] = __float_as_uint(17.0f);  // draws per sample before any is seen
     rs.col[r] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1663,16 +1671,16 @@ __global__ void __launch_bounds__(1024) k_rs_plan(RenderArgs a, RowSpec rs)
         const uint32_t x = rs.x[r];
         uint32_t t = 0;  // end of the previous window
         float mean = 0.0f, e0 = 0.0f, E = 0.0f;
-        if (x < (uint32_t)a.W) {
+        if (x < (uint32_t)rs.cw) {
             const uint32_t k = rs.k[r];
             mean = __uint_as_float(rs.prev_mean[r]);
             if (k > 0) mean = fmaxf(mean, (float)rs.pdraws[r] / (float)k);
-            e0 = (float)((uint32_t)a.spp - k) * mean * 0.5f;  // expected units to this pixel's end
-            E = (float)a.spp * mean * 0.5f;                   // ... of one whole pixel
+            e0 = (float)((uint32_t)rs.cspp - k) * mean * 0.5f;  // expected units to this pixel's end
+            E = (float)rs.cspp * mean * 0.5f;                   // ... of one whole pixel
         }
         for (int i = 0; i < rs.nwin; ++i) {
             uint32_t w = 0, s = 0;
-            if (x + (uint32_t)i < (uint32_t)a.W) {
+            if (x + (uint32_t)i < (uint32_t)rs.cw) {
                 const float ci = i == 0 ? 0.0f : e0 + (float)(i - 1) * E;
                 const float ui = i == 0 ? 0.0f : rs.spread * sqrtf((float)i) * E;
                 const float ce = e0 + (float)i * E, ue = rs.spread * sqrtf((float)(i + 1)) * E;
@@ -1723,7 +1731,7 @@ __global__ void __launch_bounds__(256) k_rs_fill(RenderArgs a, RowSpec rs, const
     int i = 0;
     for (; i + 1 < rs.nwin && l >= rs.win[i * rs.nrows + lo]; ++i) l -= rs.win[i * rs.nrows + lo];
     const uint32_t j = rs.ws[i * rs.nrows + lo] + l;
-    upix[u] = (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo] + (uint32_t)i;
+    upix[u] = rs.cpix ? rs.cpix[lo] : (uint32_t)(rs.row0 + lo) * (uint32_t)a.W + rs.x[lo] + (uint32_t)i;
     ustate[u] = sample_seed(jt2, j, rs.rng[lo]);
 }
 
@@ -1753,11 +1761,11 @@ __global__ void __launch_bounds__(64) k_rs_chase(RenderArgs a, RowSpec rs, const
             rays += (w >> kRsDrawBits) & 31u;
             erays += w >> 28;
             pdraws += draws;
-            if (listing) rs.scratch[(size_t)r * rs.scap + nl++] = make_uint2(idx, k);
+            if (listing) rs.scratch[(size_t)r * rs.scap + nl++] = make_uint2(idx, (uint32_t)rs.smp0 + k);
             else col = col + mk(t.x, t.y, t.z);  // col += Trace(...), main.cpp:218
             last = idx;
             j += draws >> 1;
-            if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
+            if (++k == (uint32_t)rs.cspp) {  // the rest of this window belongs to this pixel: dropped
                 if (!listing) out[(size_t)(rs.row0 + r) * a.W + x] = pack_pixel(col, a.spp_recip);
                 rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
                 ++x;
@@ -1836,10 +1844,10 @@ __global__ void __launch_bounds__(64) k_rs_chase_lds(RenderArgs a, RowSpec rs, c
             rays += (w >> kRsDrawBits) & 31u;
             erays += w >> 28;
             pdraws += draws;
-            s_l[nl++] = make_uint2(idx, k);
+            s_l[nl++] = make_uint2(idx, (uint32_t)rs.smp0 + k);
             last = idx;
             j += draws >> 1;
-            if (++k == (uint32_t)a.spp) {  // the rest of this window belongs to this pixel: dropped
+            if (++k == (uint32_t)rs.cspp) {  // the rest of this window belongs to this pixel: dropped
                 rs.prev_mean[r] = __float_as_uint((float)pdraws / (float)k);
                 ++x;
                 k = 0;
@@ -2232,6 +2240,35 @@ int render_wavefront(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count)
     return 0;
 }
 
+// The heaviest pixels of a pixel-seeded frame as speculative chains
+// (render_rowspec's engine with a chain = one pixel): pixel cpix[r], its
+// samples smp0 .. smp0 + cspp - 1, from the state the pilot pass left in
+// cinit[pixel] (colour sum of samples 0 .. smp0-1, RNG state in .w).
+struct PixelChains {
+    const uint32_t* cpix;
+    const float4* cinit;
+    int n, smp0, cspp;
+};
+int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters,
+                   const PixelChains* ch = nullptr);
+
+// The chains' pixels: the pilot's colour sum, then samples smp0 .. spp-1 from
+// the colour buffer, in sample order (main.cpp:218), packed (main.cpp:221-233).
+__global__ void __launch_bounds__(256) k_resolve_chains(PixelChains ch, const float4* __restrict__ sbuf, int32_t spp,
+                                                        float spp_recip, uint32_t* __restrict__ out)
+{
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= ch.n) return;
+    const uint32_t p = ch.cpix[r];
+    const float4 c0 = ch.cinit[p];
+    f3 col = mk(c0.x, c0.y, c0.z);
+    for (int32_t k = ch.smp0; k < spp; ++k) {
+        const float4 c = sbuf[(size_t)p * (size_t)spp + (size_t)k];
+        col = col + mk(c.x, c.y, c.z);
+    }
+    out[p] = pack_pixel(col, spp_recip);
+}
+
 // Persistent path engine: one launch per frame (shard).
 int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
@@ -2435,9 +2472,35 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     a2.prog = state;
     pc.cost_out = nullptr;
     pc.order = which ? tvals : vals;
+    // Pixel chains (low load): at about one pixel per resident lane the frame
+    // ends on the sample chains of its heaviest pixels.
+    // The `chains` heaviest per 1024 (the head of the cost order) leave pass 2
+    // and run as speculative chains instead -- render_rowspec's engine with one
+    // pixel per chain: every even RNG offset of a window past the pilot's state
+    // traced shadow-free, the chain walked through it, its samples traced again
+    // in full -- so their samples run side by side, not in sequence.  Same
+    // image: each sample is a pure function of (pixel, start state), summed in
+    // sample order after the pilot's sum (k_resolve_chains).  Option pixel_chains.
+    int64_t nch = 0;
+    {
+        int per1024 = help ? 16 : 0;
+        if (o.pixel_chains >= 0) per1024 = o.pixel_chains;
+        nch = std::min<int64_t>(P, (P * per1024 + 1023) / 1024);
+    }
+    if (nch > 0) {
+        const PixelChains ch{pc.order, state, (int)nch, pilot, a.spp - pilot};
+        const int rc = render_rowspec(s, a, d_out, d_counters, &ch);
+        if (rc < 0) return rc;
+        if (rc == 0) {  // pass 2 takes the rest of the order
+            pc.order += nch;
+            pc.P = P - nch;
+            pc.nchunks = (uint32_t)((pc.P + pc.chunk - 1) / pc.chunk);
+        }
+        s.chain_pixels = rc == 0 ? nch : 0;
+    }
     if (pair > 0 && pair < 64 && pc.chunk == 64u) {
         uint32_t* paired = which ? vals : tvals;
-        k_pair_order<<<(unsigned)((P + 255) / 256), 256, 0, s.stream>>>(pc.order, P, pair, paired);
+        k_pair_order<<<(unsigned)((pc.P + 255) / 256), 256, 0, s.stream>>>(pc.order, pc.P, pair, paired);
         pc.order = paired;
     }
     // SIMD-balanced first chunks (PathCtl::simd_reg): with the chunks in
@@ -2687,9 +2750,13 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
 // are split into G groups, each iterating on its own stream, so one group's
 // k_path tail overlaps another's work; the unit counts stay on the device and
 // the host only checks for completion every kCheck iterations.
-int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
+int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters,
+                   const PixelChains* ch)
 {
     const Options& o = s.opt;
+    // rows: a.tile_rows chains of W pixels x spp samples; pixel chains (ch):
+    // ch->n chains of one pixel x ch->cspp samples
+    const int cspp = ch ? ch->cspp : a.spp;
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2, kCheck = 64;
     auto fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
     // the shadow-free pass: its own instantiation (no shadow, light or colour
@@ -2698,12 +2765,12 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     auto fn3 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 3>;
     const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     const int grid3 = occupancy_grid((const void*)fn3, kBlk, 0, s.device);
-    const int rows = a.tile_rows;
+    const int rows = ch ? ch->n : a.tile_rows;
     // window cap: one iteration covers a pixel's samples at up to 2 * wmax / spp
     // = 48 draws per sample (the stand-in sponza averages ~17, its deepest rows
     // ~25; a cap of 24 draws left those rows one short window per pixel, and
     // the slowest row sets the iteration count)
-    uint32_t wmax = (uint32_t)std::min<int64_t>(8192, std::max<int64_t>(64, (int64_t)a.spp * 24));
+    uint32_t wmax = (uint32_t)std::min<int64_t>(8192, std::max<int64_t>(64, (int64_t)cspp * 24));
     if (o.rowspec_wmax > 0) wmax = (uint32_t)o.rowspec_wmax;
     // row groups, each on its own stream (one group: 3 % slower)
     const int G = std::max(1, std::min(std::min(o.rowspec_groups, kRowSpecMaxGroups), rows));
@@ -2722,24 +2789,28 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // suzanne 88 -> 51 ms with 8 -> 32 windows; the 1/8 shard of the bench
     // frame 708 ms with 8 windows, 746 with 18.
     const int64_t lanes = (int64_t)pgrid * kBlk;
-    const double E_est = (double)a.spp * 8.5;
+    const double E_est = (double)cspp * 8.5;
     int nwin = (int)std::lround(std::min((double)lanes * 5.0 / ((double)rows * E_est), 4400.0 / E_est));
     nwin = std::max(2, std::min(kRsMaxWin, nwin));
     if (o.rowspec_windows > 0) nwin = std::min(kRsMaxWin, o.rowspec_windows);
+    if (ch) nwin = 1;  // a pixel chain has one pixel: no lookahead windows
     const uint32_t jmax = (uint32_t)nwin * wmax;  // window i ends by (i + 1) * wmax
     // Speculate without shadow traversals and re-trace the chain in full at the
     // end (the frame's chain list and colour buffer must fit; else the colours
     // come from the speculative pass).  Bench frame 3.03 -> 2.49 s, 1/8 shard
     // 0.71 -> 0.61 s (profiles/r02_rowspec/rs19).  Option rowspec_noshadow.
-    bool noshadow = o.rowspec_noshadow != 0;
-    const size_t lcap = (size_t)a.slots * (size_t)a.spp;  // chain samples of the tile
-    const uint32_t scap = (uint32_t)nwin * (uint32_t)a.spp;  // a row's chain samples per iteration
+    bool noshadow = o.rowspec_noshadow != 0 || ch;
+    // chain samples of the tile (pixel chains: theirs); the colour buffer is
+    // the tile's [pixel][sample] in either case
+    const size_t lcap = ch ? (size_t)ch->n * (size_t)cspp : (size_t)a.slots * (size_t)a.spp;
+    const uint32_t scap = (uint32_t)nwin * (uint32_t)cspp;  // a row's chain samples per iteration
     if (noshadow) {
         const size_t lneed = lcap * 3 * sizeof(uint32_t) + (size_t)rows * scap * sizeof(uint2) + 256;
-        const size_t sneed = lcap * sizeof(float4);
+        const size_t sneed = (size_t)a.slots * (size_t)a.spp * sizeof(float4);
         size_t fr = 0, tot = 0;
         const size_t budget = (hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0) + s.rs_list_bytes + s.sbuf_bytes;
         if (lcap >= (1ull << 32) || lneed + sneed > budget) {
+            if (ch) return 1;  // pixel chains need the re-trace: the caller renders them in pass 2
             noshadow = false;  // does not fit: the colours come from the speculative pass
         } else {
             if (s.rs_list_bytes < lneed) {
@@ -2890,6 +2961,11 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.rs.scratch = scratch ? scratch + (size_t)q.rs.row0 * scap : nullptr;
         q.rs.scap = scap;
         q.rs.planned = spec_ctr + 8;
+        q.rs.cpix = ch ? ch->cpix + q.rs.row0 : nullptr;
+        q.rs.cinit = ch ? ch->cinit : nullptr;
+        q.rs.cw = ch ? 1 : a.W;
+        q.rs.cspp = cspp;
+        q.rs.smp0 = ch ? ch->smp0 : 0;
     }
     // the groups start after the work already on the scene's stream (the
     // caller's wait), and that stream resumes after all of them
@@ -2904,10 +2980,10 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // the listing pass's chase walks in LDS (one wave per row) when a row's
     // chain samples of one iteration fit its list; option rowspec_chase 0 = the
     // one-thread-per-row kernel
-    const bool chase_lds = noshadow && o.rowspec_chase != 0 && (uint64_t)nwin * (uint64_t)a.spp <= kChaseList;
+    const bool chase_lds = noshadow && o.rowspec_chase != 0 && (uint64_t)nwin * (uint64_t)cspp <= kChaseList;
     int it = 0;
     // every iteration moves each unfinished row by >= 1 sample, so W * spp bounds them
-    const int64_t max_it = (int64_t)a.W * a.spp + kCheck;
+    const int64_t max_it = (int64_t)(ch ? 1 : a.W) * cspp + kCheck;
     bool done = false;
     while (!done && it < max_it) {
         for (int c = 0; c < kCheck; ++c, ++it)
@@ -2957,7 +3033,12 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         pc2.sb_sp = (uint32_t)a.spp;
         TMPT_HIP(hipMemsetAsync(gs[0].heads, 0, head_words * 4, s.stream));
         fn<<<pgrid, kBlk, 0, s.stream>>>(view(s), as, pc2, d_out, gs[0].ovf, spec_ctr + 16);
-        k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(s.sbuf, a.slots, a.spp, a.spp_recip, d_out);
+        if (ch)
+            k_resolve_chains<<<(unsigned)((ch->n + 255) / 256), 256, 0, s.stream>>>(*ch, s.sbuf, a.spp, a.spp_recip,
+                                                                                   d_out);
+        else
+            k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(s.sbuf, a.slots, a.spp, a.spp_recip,
+                                                                                d_out);
         TMPT_HIP(hipGetLastError());
     }
     s.path_launches = it;
@@ -3133,6 +3214,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.extend_launches = s.shadow_launches = s.iterations = 0;
     s.row_engine = 0;
     s.stream_fallbacks = 0;
+    s.chain_pixels = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
