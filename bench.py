@@ -185,7 +185,7 @@ def counter_record() -> dict:
     return rec
 
 
-def roofline(queries: float, launch_ms: float, b_ray: float, kernel: str) -> dict:
+def roofline(queries: float, launch_ms: float, b_ray: float, kernel: str, counters_apply: bool = True) -> dict:
     """Ceilings of the dominant kernel, each as achieved / peak over the live
     launch time (the bound is the resource that binds, from
     counters; the SURVEY §8d algorithmic bytes are reported beside it):
@@ -196,7 +196,9 @@ def roofline(queries: float, launch_ms: float, b_ray: float, kernel: str) -> dic
     bytes (48 + 64 N_node + 36 N_tri per query, instrumented run) are served by
     L1 / L2 (hit rates in the record), so against HBM they are not a bound."""
     t = launch_ms * 1e-3
-    rec = counter_record()
+    # the record's per-query counts are the sample-seeding k_path's (SAMP=1);
+    # another seeding runs other kernels, so its ceilings are not given
+    rec = counter_record() if counters_apply else {}
     alg = {"bytes_per_query": round(b_ray, 1), "tbps": round(b_ray * queries / t / 1e12, 3),
            "frac_of_l2_peak": round(b_ray * queries / t / L2_PEAK_BPS, 4),
            "frac_of_hbm_peak": round(b_ray * queries / t / (HBM_PEAK_GBS * 1e9), 4),
@@ -205,7 +207,9 @@ def roofline(queries: float, launch_ms: float, b_ray: float, kernel: str) -> dic
            "algorithmic": alg}
     if not rec:
         out.update({"bound": "hbm", "achieved": round(alg["tbps"] * 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": alg["frac_of_hbm_peak"], "traffic": None})
+                    "frac": alg["frac_of_hbm_peak"], "traffic": None,
+                    "counter_ceilings": "not applicable: the counter record is the sample-seeding k_path's"
+                    if not counters_apply else "no counter record"})
         return out
     pq = rec["per_query"]
     valu_rate = pq["valu_insts"] * queries / t
@@ -480,10 +484,12 @@ def main() -> None:
         n_node = (cs.node_visits + cs.shadow_node_visits) / q
         n_tri = (cs.tri_tests + cs.shadow_tri_tests) / q
         b_ray = S_RAY + S_NODE * n_node + S_TRI * n_tri
-        kernel = ("k_path (persistent: closest-hit + shadow queries + shading)" if args.seed_mode != "row" else
-                  "speculative row engine: k_path<SAMP=2> per iteration; reference-chain rays only "
-                  "(the speculative traces are ~13x as many)")
-        roof = roofline((ext_rays + sh_rays) / ext_launches, ext_ms / ext_launches, b_ray, kernel)
+        kernel = {"sample": "k_path<SAMP=1> (persistent: closest-hit + shadow queries + shading, sample units)",
+                  "pixel": "k_path<SAMP=0> (persistent, pixel chains; pilot + cost-ordered pass)",
+                  "row": "streaming row engine: k_path<SAMP=4> speculative launch + k_path<SAMP=2> chain re-trace; "
+                         "reference-chain rays only (the speculative traces are ~11x as many)"}[args.seed_mode]
+        roof = roofline((ext_rays + sh_rays) / ext_launches, ext_ms / ext_launches, b_ray, kernel,
+                        counters_apply=args.seed_mode == "sample")
         roof.update({"n_node_per_query": round(n_node, 2), "n_tri_per_query": round(n_tri, 2)})
 
     # ---- CPU baseline: the reference algorithm on this host, bounded row sample

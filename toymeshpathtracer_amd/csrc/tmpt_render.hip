@@ -255,7 +255,8 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         if (sv.oct && !octree_root_hit(sv, o, d, t0, t1)) {
             if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
         } else {
-            id = traverse<ANY, false, BLOCK, SL, false, SOA>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
+            // a per-ray range may start behind the origin: sign-aware slack (NEG)
+            id = traverse<ANY, false, BLOCK, SL, false, SOA, RANGED>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
         }
         ids[i] = id;
         if (id >= 0) {

@@ -189,7 +189,11 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
 // KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a voted
 // round), so the other kind's code is not emitted.  TOPC: node indices below
 // st.ntop are read from the block's LDS copy of the top levels.
-template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0, bool SOA = false>
+// NEG: the query's range may reach behind the origin (the batched HitScene's
+// per-ray ranges): the far-distance slack is applied by magnitude, so it
+// widens a box's interval for negative distances too (kTfarSlack alone would
+// shrink it there); the path engines' range kMinT..kMaxT never needs it.
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0, bool SOA = false, bool NEG = false>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt, float tlo = 0.0f, float tmin = kMinT,
@@ -254,7 +258,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         for (int k = 0; k < 4; ++k) {
             float tn = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], tlo));
             float tf = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], ts.bt));
-            key[k] = tn <= tf * kTfarSlack ? tn : INFINITY;
+            const float tf_slack = NEG ? tf + fabsf(tf) * (kTfarSlack - 1.0f) : tf * kTfarSlack;
+            key[k] = tn <= tf_slack ? tn : INFINITY;
         }
         {  // nearest child next; the others pushed pairwise-ordered only
             const bool s01 = key[1] < key[0], s23 = key[3] < key[2];
@@ -481,7 +486,7 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
 // Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:86-97).
 // Returns the original triangle index or -1; (bt, bu, bv) of the hit.  TOPC:
 // the caller's block holds the top BVH levels in LDS (st.top).
-template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false, bool SOA = false>
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false, bool SOA = false, bool NEG = false>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
                                         float tmax, float& bt, float& bu, float& bv,
                                         TravStack<BLOCK, SL>& st, TravCount& cnt)
@@ -490,7 +495,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
     trav_init(ts, tmax);
     if (sv.n > 0 && !ray_has_nan(r.o, r.d)) {
         const float tlo = fminf(tmin, 0.0f);
-        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
+        while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA, NEG>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
         if (!ANY) settle_closest(sv, r.o, r.d, tmin, tmax, ts);
     }
