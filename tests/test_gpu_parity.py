@@ -100,7 +100,9 @@ def test_hitscene_kat(gpu, name):
     assert (ids >= 0).sum() > 1000
     _same_answers(ids, hits, *_ref_oracle(tris, bmin, bmax).hit_batch(rays, 0.001, 1.0e7))
     ties, roots = KAT_REFERENCE_DEVIATIONS[name]
-    assert st.tie_rule == 0 and st.tie_queries >= ties and (st.root_misses > 0) == (roots > 0)
+    # every query the octree decided is counted: ties (>= the ones whose answer
+    # changes) and root-box rejections (>= the ones the BVH would have hit)
+    assert st.tie_rule == 0 and st.tie_queries >= ties and st.root_misses >= roots
     # any-hit: same hit/miss bit
     aids, _ = sc.hit_scene_batch(rays, 0.001, 1.0e7, any_hit=True)
     assert np.array_equal(aids >= 0, ids >= 0)

@@ -393,6 +393,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.nodes4) (void)hipFree(s.nodes4);
     if (s.oct) (void)hipFree(s.oct);
     if (s.oct_refs) (void)hipFree(s.oct_refs);
+    if (s.oct_view) (void)hipFree(s.oct_view);
     if (s.soa_buf) (void)hipFree(s.soa_buf);
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
@@ -452,6 +453,17 @@ int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax
         return -1;
     }
     if (s.stream) (void)hipStreamSynchronize(s.stream);  // a render in flight may still read the old one
+    if (!s.oct_view && hipMalloc(&s.oct_view, sizeof(OctView)) != hipSuccess) {
+        (void)hipFree(d_nodes);
+        (void)hipFree(d_refs);
+        return (set_error("tmpt_scene_build_octree: out of device memory"), -1);
+    }
+    const OctView ov{d_nodes, d_refs, (int32_t)t.nodes.size(), s.ties};
+    if (hipMemcpy(s.oct_view, &ov, sizeof(ov), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d_nodes);
+        (void)hipFree(d_refs);
+        return (set_error("tmpt_scene_build_octree: upload failed"), -1);
+    }
     if (s.oct) (void)hipFree(s.oct);
     if (s.oct_refs) (void)hipFree(s.oct_refs);
     s.oct = d_nodes;

@@ -667,7 +667,7 @@ __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tr
     f3 e1 = v1 - v0, e2 = v2 - v0;  // maths.cpp:341-342, same roundings
     pre[k].a = f4(v0.x, v0.y, v0.z, e1.x);
     pre[k].b = f4(e1.y, e1.z, e2.x, e2.y);
-    pre[k].c = f4(e2.z, __int_as_float(o), 0.0f, 0.0f);
+    pre[k].c = f4(e2.z, __int_as_float(2 * o), 0.0f, 0.0f);  // doubled: TravState::best's tie bit is bit 0
 }
 
 inline int blocks_for(int64_t n, int b) { return (int)((n + b - 1) / b); }

@@ -45,7 +45,7 @@ constexpr int kTopNodes = 120;  // BVH4 nodes held in LDS per path block (7.5 KB
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x
     float4 b;  // e1.yz, e2.xy
-    float4 c;  // e2.z, original index (int bits), 0, 0
+    float4 c;  // e2.z, 2 x original index (int bits; bit 0 is the traversal's tie flag), 0, 0
 };
 struct alignas(16) TriOrig {
     float4 a;  // v0.xyz, v1.x
@@ -68,6 +68,16 @@ struct alignas(16) OctNode {
     float4 hi;
 };
 static_assert(sizeof(OctNode) == 32, "octree node: two dwordx4 loads");
+
+// What the kernels see of it (one device-side struct, so a kernel keeps one
+// pointer live): nodes, leaf lists, node count, the counters of the queries
+// it answered ([0] ties, [1] root-box misses; Scene::ties).
+struct OctView {
+    const OctNode* nodes;
+    const int32_t* refs;
+    int32_t n;
+    unsigned long long* ties;
+};
 
 struct OctreeHost {
     std::vector<OctNode> nodes;
@@ -169,6 +179,7 @@ struct Scene {
     // closest-hit queries answered through it in the current call
     OctNode* oct = nullptr;
     int32_t* oct_refs = nullptr;
+    OctView* oct_view = nullptr;  // device copy of {oct, oct_refs, n_oct, ties}
     int32_t n_oct = 0, oct_leaves = 0, oct_depth = 0;
     int64_t n_oct_refs = 0;
     double oct_build_ms = 0.0;

@@ -135,7 +135,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
         float t, u, v;
         int id = -1;
         if (depth == 0 && root_check && !octree_root_hit(sv, o, d, kMinT, kMaxT)) {
-            if (sv.ties) atomicAdd(&sv.ties[1], 1ull);  // the camera ray misses the reference's root box
+            atomicAdd(&sv.oct->ties[1], 1ull);  // the camera ray misses the reference's root box
         } else {
             id = mega_query<false, COUNT, TOPC>(sv, o, d, t, u, v, st, cnt);
         }
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         int id = -1;
         // with the reference's octree: its root box test first (scene.cpp:25)
         if (sv.oct && !octree_root_hit(sv, o, d, t0, t1)) {
-            if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
+            atomicAdd(&sv.oct->ties[1], 1ull);
         } else {
             // a per-ray range may start behind the origin: sign-aware slack (NEG)
             id = traverse<ANY, false, BLOCK, SL, false, SOA, RANGED>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                     steps = 0;
                     const bool root_miss = !ANY && s.root_check && s.depth[p] == 0 &&
                                            !octree_root_hit(sv, o, d, kMinT, kMaxT);
-                    if (root_miss && sv.ties) atomicAdd(&sv.ties[1], 1ull);
+                    if (root_miss) atomicAdd(&sv.oct->ties[1], 1ull);
                     if (sv.n > 0 && !ray_has_nan(o, d) && !root_miss) {
                         active = true;
                     } else if (!ANY) {  // provably no hit (NaN ray, empty scene, root box): a counted miss
@@ -1195,9 +1195,14 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 ps_t = stamp();
                 ps_fetch += ps_t - pt_t;
             }
-            {  // closest hits tied on t: the reference's pick (settle_closest; rare, wave-uniform skip)
-                const bool tie = has_pix && !in_query && !cam && !qany && ts.best >= 0 && (ts.best & kTieBit) != 0;
-                if (wany(tie) && tie) settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
+            {  // finished closest hits: the triangle index, ties answered by the octree
+                // (settle_closest, split so the rare octree walk sits behind a wave-uniform skip)
+                const bool fin = has_pix && !in_query && !cam && !qany;
+                const bool tie = fin && octree_tie(sv, ts);
+                if (wany(tie)) {
+                    if (tie) settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
+                }
+                if (fin && !tie) ts.best >>= 1;
             }
             // ---- finished queries: shade
             bool finish = false, want_off = false;
@@ -1400,7 +1405,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
                 if (a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
                     in_query = false;  // a camera ray outside the reference's root box: a counted miss
-                    if (sv.ties) atomicAdd(&sv.ties[1], 1ull);
+                    atomicAdd(&sv.oct->ties[1], 1ull);
                 }
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
@@ -1969,10 +1974,7 @@ SceneView view(const Scene& s)
     SceneView v{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4};
     v.soa = s.soa;
     if (s.oct && s.opt.tie_rule == 0) {  // the reference's visit order for ties
-        v.oct = s.oct;
-        v.oct_refs = s.oct_refs;
-        v.n_oct = s.n_oct;
-        v.ties = s.ties;
+        v.oct = s.oct_view;
     }
     return v;
 }
@@ -2484,7 +2486,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // sample order after the pilot's sum (k_resolve_chains).  Option pixel_chains.
     int64_t nch = 0;
     {
-        int per1024 = help ? 16 : 0;
+        int per1024 = 0;  // measured: no gain at the 1/8 shard, so off by default
         if (o.pixel_chains >= 0) per1024 = o.pixel_chains;
         nch = std::min<int64_t>(P, (P * per1024 + 1023) / 1024);
     }
@@ -2986,8 +2988,11 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
     // every iteration moves each unfinished row by >= 1 sample, so W * spp bounds them
     const int64_t max_it = (int64_t)(ch ? 1 : a.W) * cspp + kCheck;
     bool done = false;
+    // pixel chains finish in a few iterations: the host looks after each one
+    // (an empty iteration still launches the persistent grid, ~0.3 ms)
+    const int check = ch ? 1 : kCheck;
     while (!done && it < max_it) {
-        for (int c = 0; c < kCheck; ++c, ++it)
+        for (int c = 0; c < check; ++c, ++it)
             for (Group& q : gs) {
                 k_rs_plan<<<1, 1024, 0, q.st>>>(a, q.rs);
                 k_rs_fill<<<(unsigned)((q.U + 255) / 256), 256, 0, q.st>>>(a, q.rs, s.jt2, q.upix, q.ustate);

@@ -9,7 +9,7 @@
 //   distance), so the Moller-Trumbore test alone -- bit-identical to
 //   maths.cpp:339-380 -- decides every hit.  When two or more triangles share
 //   the closest t, the lowest index is kept and the query is flagged
-//   (kTieBit in TravState::best): the reference keeps the first of them in its
+//   (bit 0 of TravState::best): the reference keeps the first of them in its
 //   octree's visit order (scene.cpp:29-48), so with the scene's octree built
 //   (tmpt_scene_build_octree) a flagged query is answered again over that
 //   octree, exactly as HitSceneInternal walks it (octree_closest below).
@@ -134,21 +134,14 @@ struct SceneView {
     const TriOrig* __restrict__ tri_orig;
     int32_t n;
     int32_t n_nodes4 = 0;
-    // the reference's octree (null: none built, or option tie_rule = index) and
-    // the counters of the queries it answered ([0] ties, [1] root-box misses)
-    const OctNode* __restrict__ oct = nullptr;
-    const int32_t* __restrict__ oct_refs = nullptr;
-    int32_t n_oct = 0;
-    unsigned long long* ties = nullptr;
+    // the reference's octree (null: none built, or option tie_rule = index):
+    // one pointer to its device-side view, read only by the rare flagged
+    // queries (the kernels keep one SGPR pair live for it, not four)
+    const OctView* __restrict__ oct = nullptr;
     // build option layout=soa (tmpt_internal.h SoaScene): the same nodes and
     // triangle records as planes, read by the SOA instantiations
     SoaScene soa;
 };
-
-// TravState::best of a closest-hit query whose t is shared by two or more
-// triangles (the lowest index among them in the low bits)
-constexpr int kTieBit = 1 << 30;
-constexpr int kIdMask = kTieBit - 1;
 
 struct TravCount {
     uint32_t nodes = 0, tris = 0;
@@ -158,8 +151,9 @@ struct TravCount {
 struct TravState {
     int node;   // next node (>=0 internal, <0 leaf = ~slot)
     int sp;     // stack depth
-    int best;   // original triangle index of the current closest hit, -1 if none;
-                // | kTieBit when another triangle was accepted at the same t
+    int best;   // during traversal: 2 x the triangle index of the current closest hit
+                // (TriPre stores it doubled), | 1 when another triangle was accepted at
+                // the same t; -1 if none.  settle_closest turns it into the index.
     float bt, bu, bv;
 };
 
@@ -179,7 +173,7 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
 // slots carry an inverted box and link to the null leaf); the nearest hit
 // child is next, the others are pushed pairwise-ordered.  Leaf: its triangles'
 // Moller-Trumbore tests (bit-exact, maths.cpp:339-380) with t in [tmin, tmax];
-// ties on t keep the lowest triangle index and set kTieBit (the caller settles
+// ties on t keep the lowest triangle index and set bit 0 (the caller settles
 // them, settle_closest).  `any` (run time): stop at the
 // first accepted triangle (the shadow query).  Returns true when the query is
 // finished; ts.node is undefined after that (the next query re-inits it).
@@ -288,16 +282,18 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             float t, u, v;
             if (mt_test(r.o, r.d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c.x), tmin, tmax,
                         t, u, v)) {
-                int id = __float_as_int(c.y);
+                // id = 2 x index: comparing it with best (2 x index | tie bit)
+                // orders the indices; the tie bit never decides
+                const int id = __float_as_int(c.y);
                 const bool tie = t == ts.bt && ts.best >= 0;
-                if (t < ts.bt || (tie && id < (ts.best & kIdMask))) {
+                if (t < ts.bt || (tie && id < ts.best)) {
                     ts.bt = t;
                     ts.bu = u;
                     ts.bv = v;
-                    ts.best = id | (tie ? kTieBit : 0);
+                    ts.best = id | (int)tie;
                     if (any) return true;
-                } else if (tie) {
-                    ts.best |= kTieBit;
+                } else {
+                    ts.best |= (int)tie;
                 }
             }
             return false;
@@ -336,17 +332,17 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                              n > 1u;
             const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
             const bool tie0 = ok0 && t0 == ts.bt && ts.best >= 0;
-            const bool acc0 = ok0 && (t0 < ts.bt || (tie0 && id0 < (ts.best & kIdMask)));
+            const bool acc0 = ok0 && (t0 < ts.bt || (tie0 && id0 < ts.best));
             ts.bt = acc0 ? t0 : ts.bt;
             ts.bu = acc0 ? u0 : ts.bu;
             ts.bv = acc0 ? w0 : ts.bv;
-            ts.best = (acc0 ? id0 : ts.best) | (tie0 ? kTieBit : 0);
+            ts.best = (acc0 ? id0 : ts.best) | (int)tie0;
             const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt && ts.best >= 0;
-            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (tie1 && id1 < (ts.best & kIdMask)));
+            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (tie1 && id1 < ts.best));
             ts.bt = acc1 ? t1 : ts.bt;
             ts.bu = acc1 ? u1 : ts.bu;
             ts.bv = acc1 ? w1 : ts.bv;
-            ts.best = (acc1 ? id1 : ts.best) | (tie1 ? kTieBit : 0);
+            ts.best = (acc1 ? id1 : ts.best) | (int)tie1;
             if (any && (acc0 || acc1)) return true;
         } else {  // a lone lane (row chains) gains more from the early exits
             if (tri(a0, b0, c0)) return true;
@@ -407,7 +403,7 @@ __device__ __forceinline__ f3 ref_inverse(f3 d) { return mk(1.0f / d.x, 1.0f / d
 // them on the root's boundary).
 __device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax)
 {
-    return ref_slab(o, ref_inverse(d), sv.oct[0].lo, sv.oct[0].hi, tmin, tmax);
+    return ref_slab(o, ref_inverse(d), sv.oct->nodes[0].lo, sv.oct->nodes[0].hi, tmin, tmax);
 }
 
 // HitSceneInternal (scene.cpp:21-52) over the preorder octree: a node whose
@@ -423,17 +419,20 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
     const f3 inv = ref_inverse(d);
     int best = -1;
     float tb = tmax, ub = 0.0f, vb = 0.0f;
-    for (int i = 0; i < sv.n_oct;) {
-        const float4 lo = sv.oct[i].lo, hi = sv.oct[i].hi;
+    const OctNode* __restrict__ nodes = sv.oct->nodes;
+    const int32_t* __restrict__ refs = sv.oct->refs;
+    const int n_oct = sv.oct->n;
+    for (int i = 0; i < n_oct;) {
+        const float4 lo = nodes[i].lo, hi = nodes[i].hi;
         if (!ref_slab(o, inv, lo, hi, tmin, tmax)) {
             i = __float_as_int(lo.w);
             continue;
         }
         const int ref = __float_as_int(hi.w);
         if (ref >= 0) {
-            const int cnt = sv.oct_refs[ref];
+            const int cnt = refs[ref];
             for (int k = 1; k <= cnt; ++k) {
-                const int id = sv.oct_refs[ref + k];
+                const int id = refs[ref + k];
                 const float4* p = reinterpret_cast<const float4*>(sv.tri_orig + id);
                 const float4 a = p[0], b = p[1], c = p[2];
                 const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
@@ -454,19 +453,24 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
     return best;
 }
 
-// A finished closest-hit query: a flagged tie is answered again over the
-// octree (the reference's pick among the tied triangles, and its whole answer
-// for that ray); without an octree the lowest index stands.
+// Whether a finished closest-hit query is a flagged tie the octree answers.
+__device__ __forceinline__ bool octree_tie(const SceneView& sv, const TravState& ts)
+{
+    return sv.oct != nullptr && ts.best >= 0 && (ts.best & 1) != 0;
+}
+
+// A finished closest-hit query: the triangle index from TravState::best; a
+// flagged tie is answered again over the octree (the reference's pick among
+// the tied triangles, and its whole answer for that ray); without an octree
+// the lowest index stands.
 __device__ __forceinline__ void settle_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
                                                TravState& ts)
 {
-    if (ts.best >= 0 && (ts.best & kTieBit)) {
-        if (sv.oct) {
-            if (sv.ties) atomicAdd(&sv.ties[0], 1ull);
-            ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bu, ts.bv);
-        } else {
-            ts.best &= kIdMask;
-        }
+    if (octree_tie(sv, ts)) {
+        atomicAdd(&sv.oct->ties[0], 1ull);
+        ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bu, ts.bv);
+    } else {
+        ts.best >>= 1;  // -1 stays -1
     }
 }
 
