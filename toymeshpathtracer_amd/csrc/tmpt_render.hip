@@ -1198,11 +1198,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             {  // finished closest hits: the triangle index, ties answered by the octree
                 // (settle_closest, split so the rare octree walk sits behind a wave-uniform skip)
                 const bool fin = has_pix && !in_query && !cam && !qany;
+#ifdef TMPT_EXP_NOSETTLE  // cost experiment: no octree re-answer
+                if (fin) ts.best >>= 1;
+#else
                 const bool tie = fin && octree_tie(sv, ts);
                 if (wany(tie)) {
                     if (tie) settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
                 }
                 if (fin && !tie) ts.best >>= 1;
+#endif
             }
             // ---- finished queries: shade
             bool finish = false, want_off = false;
@@ -1341,7 +1345,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         // the unit is held in `col` (unused with a colour buffer) and
                         // written with it, back to back into one 32-B sector
                         const bool odd = (smp & 1u) != 0u;
+#ifdef TMPT_EXP_NOPAIR  // cost experiment: no paired stores
+                        if (false) {
+#else
                         if (pc.pair && !odd && smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u) {
+#endif
                             col = color;
                         } else {
                             if (pc.pair && odd) __builtin_nontemporal_store((f32x4){col.x, col.y, col.z, 0.0f}, dst - 1);
@@ -1403,10 +1411,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
+#ifndef TMPT_EXP_NOROOT  // cost experiment: no root box test
                 if (a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
                     in_query = false;  // a camera ray outside the reference's root box: a counted miss
                     atomicAdd(&sv.oct->ties[1], 1ull);
                 }
+#endif
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
         }

@@ -331,6 +331,21 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                                           mk(b1.z, b1.w, c1.x), tmin, tmax, t1, u1, w1) &&
                              n > 1u;
             const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
+#ifdef TMPT_EXP_NOTIE  // cost experiment: no tie flag (wrong answers on ties)
+            const bool tie0 = false, tie1 = false;
+            const bool acc0 = ok0 && (t0 < ts.bt || (t0 == ts.bt && ts.best >= 0 && id0 < ts.best));
+            ts.bt = acc0 ? t0 : ts.bt;
+            ts.bu = acc0 ? u0 : ts.bu;
+            ts.bv = acc0 ? w0 : ts.bv;
+            ts.best = acc0 ? id0 : ts.best;
+            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (t1 == ts.bt && ts.best >= 0 && id1 < ts.best));
+            ts.bt = acc1 ? t1 : ts.bt;
+            ts.bu = acc1 ? u1 : ts.bu;
+            ts.bv = acc1 ? w1 : ts.bv;
+            ts.best = acc1 ? id1 : ts.best;
+            (void)tie0;
+            (void)tie1;
+#else
             const bool tie0 = ok0 && t0 == ts.bt && ts.best >= 0;
             const bool acc0 = ok0 && (t0 < ts.bt || (tie0 && id0 < ts.best));
             ts.bt = acc0 ? t0 : ts.bt;
@@ -343,6 +358,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             ts.bu = acc1 ? u1 : ts.bu;
             ts.bv = acc1 ? w1 : ts.bv;
             ts.best = (acc1 ? id1 : ts.best) | (int)tie1;
+#endif
             if (any && (acc0 || acc1)) return true;
         } else {  // a lone lane (row chains) gains more from the early exits
             if (tri(a0, b0, c0)) return true;
@@ -412,9 +428,11 @@ __device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d,
 // never shrunk, scene.cpp:32) and keeps a hit only if t < the best so far
 // (scene.cpp:34), so among equal t the first met in child order 0..7 wins.
 // Returns the triangle index or -1; (t, u, v) of the hit, e1/e2 formed as
-// maths.cpp:341-342 forms them.
-__device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float& bt,
-                                           float& bu, float& bv)
+// maths.cpp:341-342 forms them.  `target`: the closest t over all triangles
+// (the BVH's answer): no triangle has a smaller one, so the first met at
+// exactly `target` is the reference's answer and the walk stops there.
+__device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float target,
+                                           float& bt, float& bu, float& bv)
 {
     const f3 inv = ref_inverse(d);
     int best = -1;
@@ -442,6 +460,10 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
                     ub = u;
                     vb = v;
                     best = id;
+                    if (t == target) {  // first at the minimum: nothing can replace it
+                        i = n_oct;
+                        break;
+                    }
                 }
             }
         }
@@ -468,7 +490,7 @@ __device__ __forceinline__ void settle_closest(const SceneView& sv, f3 o, f3 d, 
 {
     if (octree_tie(sv, ts)) {
         atomicAdd(&sv.oct->ties[0], 1ull);
-        ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bu, ts.bv);
+        ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bt, ts.bu, ts.bv);
     } else {
         ts.best >>= 1;  // -1 stays -1
     }
@@ -502,6 +524,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
         while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA, NEG>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
         if (!ANY) settle_closest(sv, r.o, r.d, tmin, tmax, ts);
+        else ts.best >>= 1;  // the doubled index of the first accepted triangle (-1 stays -1)
     }
     bt = ts.bt;
     bu = ts.bu;
