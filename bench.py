@@ -433,7 +433,13 @@ def main() -> None:
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             csteps = min(args.steps, 3)  # informational: a few frames (row seeding takes ~3 s each)
-            crays = sum(step(sd)[0] for _ in range(csteps))
+            crays = 0
+            engines, fallbacks = set(), 0
+            for _ in range(csteps):
+                r_, st_ = step(sd)
+                crays += r_
+                engines.add(st_.row_engine)
+                fallbacks += st_.stream_fallbacks
             torch.cuda.synchronize()
             if dist_on:
                 dist.barrier()
@@ -447,6 +453,10 @@ def main() -> None:
                 crays = int(r.item())
             compare[name] = {"value": round(crays / cel / 1e6, 2), "ms_per_step": round(cel / csteps * 1e3, 2),
                              "rays_per_step": crays // csteps, "steps": csteps}
+            if name == "row":  # which row engine ran, and whether the streaming launch fell back
+                compare[name].update({"row_engine": sorted({3: "streaming", 2: "iterated", 1: "lane per row"}
+                                                           .get(e, str(e)) for e in engines),
+                                      "stream_fallbacks": fallbacks})
     if rank != 0:
         scene.close()
         dist.destroy_process_group()
