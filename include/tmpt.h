@@ -32,7 +32,8 @@ extern "C" {
                               7: tmpt_scene_build_octree (the reference's octree: its answer
                               for closest hits tied on t and for rays its root box drops),
                               option tie_rule, tmpt_octree_digest, tmpt_stats octree / tie /
-                              row-engine fields, tmpt_render_multi takes the octree box */
+                              row-engine fields, tmpt_render_multi takes the octree box,
+                              options tie_defer / redo_cap, tmpt_stats.redo_samples */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -131,6 +132,7 @@ typedef struct {
     int32_t octree_depth;
     int32_t tie_rule;         /* in effect: 0 octree visit order, 1 lowest index (no octree / option) */
     int64_t chain_pixels;     /* pixel seeding: pixels the last render ran as speculative chains */
+    int64_t redo_samples;     /* sample seeding, tie_defer: samples the last render traced again */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */
@@ -215,7 +217,16 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   tie_rule         visit (0, default) | index (1): closest hits tied on t take the
  *                    reference's octree visit order (needs tmpt_scene_build_octree)
  *                    or the lowest triangle index -- the one option that can change
- *                    an answer, by design: index is the exact-semantics contract */
+ *                    an answer, by design: index is the exact-semantics contract
+ *   tie_defer        sample seeding with the colour buffer: a sample whose closest hit
+ *                    is a tie is dropped by the main loop (built without the octree
+ *                    walk) and traced again, ties settled, by the launch's waves once
+ *                    their main loop is done (-1 = auto, 0 = off: ties settled in the
+ *                    main loop, 1 = on); the image and ray counts are the same either way
+ *   redo_cap         test hook (0 = auto): the capacity of tie_defer's sample list; a
+ *                    frame that overflows it is rendered again with the list grown
+ *   redo_inline      test hook (1): 0 leaves every dropped sample to the second launch
+ *                    that otherwise takes only those the main launch's tail did not */
 int tmpt_scene_create_ex(const float* tris, int32_t n, int32_t device, const char* options, tmpt_scene** out);
 int tmpt_scene_set_option(tmpt_scene* scene, const char* key, double value);
 int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* value);

@@ -845,7 +845,8 @@ def test_sample_mode_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
     with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
         img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
-        assert sc.stats().tie_queries > 0
+        st = sc.stats()
+        assert st.tie_queries > 0 and st.redo_samples > 0  # ties left to the redo pass (tie_defer auto)
         sc.set_option("tie_rule", 1)
         img_ix, rays_ix = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
     rows = np.arange(0, h, 64)
@@ -857,6 +858,49 @@ def test_sample_mode_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
     rows = np.arange(0, h, 64)
     diff = np.nonzero((img[rows] != ref[rows]).any(-1))
     assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+
+
+@pytest.mark.parametrize("shards", [1, 8])
+def test_tie_defer_same_frame_and_rays(gpu, sponza_path, shards):
+    """Deferred ties (option tie_defer): the sample kernel's main loop, built
+    without the octree walk, drops each sample whose closest hit is a tie; the
+    launch's waves trace those samples again, ties settled, once their main
+    loop is done.  The frame and its ray count equal the render that settles
+    ties in the main loop (tie_defer=0), for the whole frame and a 1/8 shard;
+    a redo list too small for the frame (test hook redo_cap=1) overflows, and
+    the frame is rendered again with the list grown; with the tail's redo
+    phase off (test hook redo_inline=0) the k_redo launch traces them all --
+    same frame, same rays each time.  Rows every 16th
+    against the oracle octree close the loop to the reference's answers."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 480, 270, 16
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    kw = dict(seed_mode=tm.SEED_SAMPLE, band_rows=1, shard=0, num_shards=shards)
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        sc.set_option("tie_defer", 0)
+        exact, rays_exact = sc.trace_image(cam, w, h, spp, **kw)
+        st0 = sc.stats()
+        assert st0.redo_samples == 0 and st0.tie_queries > 0
+        sc.set_option("tie_defer", 1)
+        img, rays = sc.trace_image(cam, w, h, spp, **kw)
+        st1 = sc.stats()
+        assert st1.redo_samples > 0
+        assert st1.tie_queries == st0.tie_queries  # the redo pass meets the same ties
+        assert rays == rays_exact and np.array_equal(img, exact)
+        sc.set_option("redo_cap", 1)
+        img2, rays2 = sc.trace_image(cam, w, h, spp, **kw)
+        assert sc.stats().redo_samples == st1.redo_samples
+        assert rays2 == rays_exact and np.array_equal(img2, exact)
+        sc.set_option("redo_cap", 0)
+        sc.set_option("redo_inline", 0)  # every dropped sample to the k_redo launch
+        img3, rays3 = sc.trace_image(cam, w, h, spp, **kw)
+        assert sc.stats().redo_samples == st1.redo_samples
+        assert rays3 == rays_exact and np.array_equal(img3, exact)
+    if shards == 1:
+        ref, _ = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE,
+                                                      row_step=16)
+        rows = np.arange(0, h, 16)
+        assert np.array_equal(img[rows], ref[rows])
 
 
 def test_sponza4k_config4_shard_oracle_and_fallback(gpu, sponza_path):

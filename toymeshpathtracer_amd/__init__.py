@@ -102,7 +102,8 @@ class _Stats(ctypes.Structure):
                 ("octree_build_ms", ctypes.c_double), ("tie_queries", ctypes.c_uint64),
                 ("root_misses", ctypes.c_uint64), ("row_engine", ctypes.c_int32),
                 ("stream_fallbacks", ctypes.c_int32), ("octree_depth", ctypes.c_int32),
-                ("tie_rule", ctypes.c_int32), ("chain_pixels", ctypes.c_int64)]
+                ("tie_rule", ctypes.c_int32), ("chain_pixels", ctypes.c_int64),
+                ("redo_samples", ctypes.c_int64)]
 
 
 def _sig(name, res, args):
@@ -316,6 +317,7 @@ class RenderStats:
     octree_depth: int
     tie_rule: int
     chain_pixels: int
+    redo_samples: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

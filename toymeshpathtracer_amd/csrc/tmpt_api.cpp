@@ -120,6 +120,9 @@ const OptionDef kOptions[] = {
     {"dprio", false, 0, 1, &Options::dprio, nullptr, nullptr},
     {"wave_cap", false, 0, 64, &Options::wave_cap, nullptr, nullptr},
     {"pixel_chains", false, -1, 1024, &Options::pixel_chains, nullptr, nullptr},
+    {"tie_defer", false, -1, 1, &Options::tie_defer, nullptr, nullptr},
+    {"redo_cap", false, 0, 1 << 30, &Options::redo_cap, nullptr, nullptr},
+    {"redo_inline", false, 0, 1, &Options::redo_inline, nullptr, nullptr},
     {"rowspec", false, 0, 1, &Options::rowspec, nullptr, nullptr},
     {"rowspec_wmax", false, 0, 16384, &Options::rowspec_wmax, nullptr, nullptr},
     {"rowspec_windows", false, 0, 32, &Options::rowspec_windows, nullptr, nullptr},
@@ -398,6 +401,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.prog) (void)hipFree(s.prog);
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);
+    if (s.redo) (void)hipFree(s.redo);
     if (s.jt2) (void)hipFree(s.jt2);
     if (s.rs_buf) (void)hipFree(s.rs_buf);
     for (auto& st : s.rs_stream)
@@ -841,6 +845,7 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->octree_depth = s.oct_depth;
     o->tie_rule = s.oct && s.opt.tie_rule == 0 ? 0 : 1;
     o->chain_pixels = s.chain_pixels;
+    o->redo_samples = s.redo_samples;
     return 0;
 }
 

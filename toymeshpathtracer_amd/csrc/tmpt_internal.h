@@ -84,6 +84,7 @@ struct OctreeHost {
     std::vector<int32_t> refs;
     int32_t leaves = 0, depth = 0;
 };
+
 // Subdivide / InternalDivide of scene.cpp:99-160 from the root box [bmin, bmax]
 // (main.cpp:312: the scene bounds +- 0.7 x their size)
 void build_octree(const float* tris9, int32_t n, const float bmin[3], const float bmax[3], OctreeHost& out);
@@ -122,6 +123,7 @@ constexpr int kStackTotal = 128;
 constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
 constexpr int kRenderCounters = 32;   // ray / visit / round counters of one render
 constexpr int kTieCounter = 24;       // [24] tied queries re-answered over the octree, [25] root-box misses
+constexpr int kRedoCounter = 26;      // samples the deferred-tie sample kernel left to the redo pass
 
 // Per-scene options: the library's control plane in place of environment
 // variables (include/tmpt.h documents each key).  Build options are fixed when
@@ -158,6 +160,12 @@ struct Options {
     int wf_bins = 1;          // wavefront engine: extend sub-queues per segment by direction octant (1, 2, 4, 8)
     int tie_rule = 0;         // closest hits tied on t: 0 = the reference's octree visit order (needs
                               // tmpt_scene_build_octree), 1 = the lowest triangle index
+    int tie_defer = -1;       // sample seeding, octree rule: tied samples left to a redo pass, so the
+                              // main kernel carries no octree walk (-1 auto, 0 off, 1 on)
+    int redo_cap = 0;         // test hook: the redo list's capacity in entries (0 = auto; a small one
+                              // overflows, and the frame is rendered again with the list grown)
+    int redo_inline = 1;      // test hook: 0 = the deferring kernel's waves leave every dropped sample
+                              // to the k_redo launch (its fallback) instead of tracing them in their tail
 };
 int options_parse(Options& o, const char* text, bool allow_build);
 int options_set(Options& o, const char* key, double value, bool allow_build);
@@ -213,6 +221,11 @@ struct Scene {
     int32_t jt_spp = 0;
     float4* sbuf = nullptr;
     size_t sbuf_bytes = 0;
+    // deferred ties (PathCtl::redo): the redo list, its capacity in entries,
+    // and the samples the last render left to the redo pass
+    uint2* redo = nullptr;
+    uint32_t redo_cap = 0;
+    int64_t redo_samples = 0;
     // speculative row seeding (tmpt_render.hip render_rowspec): jump tables
     // M^(2j) for j in [0, jt2_n), and its row/unit buffers
     uint32_t* jt2 = nullptr;

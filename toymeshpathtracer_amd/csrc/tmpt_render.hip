@@ -65,6 +65,14 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
+// a branch taken by few waves (octree tie re-answers, root-box misses): laid out
+// away from the hot loop body
+#ifdef TMPT_EXP_COLD
+#define TMPT_RARE(x) __builtin_expect(!!(x), 0)
+#else
+#define TMPT_RARE(x) (x)
+#endif
+
 // s_memtime (shader clock), for the PROF build of k_path only
 __device__ __forceinline__ uint64_t stamp()
 {
@@ -123,9 +131,11 @@ __device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float
     return traverse<ANY, COUNT, BLOCK, SL, TOPC>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
 }
 
+// rays: closest-hit queries, srays: shadow queries (the same counter where the
+// caller does not split them)
 template <bool COUNT, int BLOCK, int SL, bool TOPC = false>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
-                                         uint32_t& rays, TravStack<BLOCK, SL>& st, float* lbuf,
+                                         uint32_t& rays, uint32_t& srays, TravStack<BLOCK, SL>& st, float* lbuf,
                                          TravCount& cnt, bool root_check)
 {
     int depth = 0;
@@ -142,7 +152,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
         if (id >= 0) {
             f3 pos, nrm;
             hit_record(sv, id, u, v, pos, nrm);
-            ++rays;  // shadow ray, main.cpp:57-59 (always counted)
+            ++srays;  // shadow ray, main.cpp:57-59 (always counted)
             float lc = light_cosine(nrm, d);
             if (lc > 0.0f) {  // a zero light term does not depend on the answer
                 float ts, us, vs;
@@ -176,9 +186,84 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
         f3 o, d;
         if (a.jt) rng = sample_seed(a.jt, (uint32_t)s, pseed);  // sample seeding
         camera_sample(a.cam, (uint32_t)x, (uint32_t)y, a.invW, a.invH, rng, o, d);
-        col = col + trace_path<COUNT, BLOCK, SL, TOPC>(sv, o, d, rng, rays, st, lbuf, cnt, a.root_check != 0);
+        col = col + trace_path<COUNT, BLOCK, SL, TOPC>(sv, o, d, rng, rays, rays, st, lbuf, cnt, a.root_check != 0);
     }
     return pack_pixel(col, a.spp_recip);
+}
+
+#ifdef TMPT_EXP_WALKSTAT
+__device__ unsigned long long g_walkstat[4];
+#endif
+
+// ============================================================ deferred ties
+// A sample the deferring sample kernel (k_path DEFER) dropped on a tied
+// closest hit, traced again whole by one lane with ties settled
+// (trace_path's queries end in settle_closest): sample `smp` of tile pixel
+// `pix` from its own seed (sample seeding, main.cpp:212-216), its colour to
+// the colour buffer, where k_resolve_px sums it in sample order.
+constexpr uint32_t kRedoEmpty = 0xFFFFFFFFu;  // a list entry not yet written
+constexpr uint32_t kRedoDone = 0xFFFFFFFEu;   // an entry already traced
+constexpr int kRedoTaken = 27, kRedoWaves = 28, kRedoTraced = 29;  // counters[]: tickets, waves past the main loop, traced
+
+template <int BLOCK, int SL>
+__device__ __forceinline__ void redo_sample(const SceneView& sv, const RenderArgs& a, uint32_t pix, uint32_t smp,
+                                            float4* __restrict__ sbuf, uint32_t sb_ss, uint32_t sb_sp,
+                                            uint32_t& rays_e, uint32_t& rays_s, TravStack<BLOCK, SL>& st, float* lbuf)
+{
+    const int lr = (int)(pix / (uint32_t)a.W);
+    const uint32_t x = pix - (uint32_t)lr * (uint32_t)a.W, y = (uint32_t)tile_row_to_y(a, lr);
+    uint32_t rng = sample_seed(a.jt, smp, pixel_seed(x, y, (uint32_t)a.W));
+    f3 o, d;
+    camera_sample(a.cam, x, y, a.invW, a.invH, rng, o, d);
+    TravCount cnt;
+    const f3 c = trace_path<false, BLOCK, SL, true>(sv, o, d, rng, rays_e, rays_s, st, lbuf, cnt, false);
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((f32x4){c.x, c.y, c.z, 0.0f},
+                                reinterpret_cast<f32x4*>(sbuf + ((size_t)smp * sb_ss + (size_t)pix * sb_sp)));
+}
+
+__device__ __forceinline__ uint2 redo_load(const uint2* p)
+{
+    const unsigned long long w =
+        __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+}
+
+__device__ __forceinline__ void redo_mark(uint2* p)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned int*>(p), kRedoDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The entries the deferring launch left untraced (its waves gave up waiting,
+// see k_path's redo phase): one lane per entry, grid-stride.
+template <int BLOCK, int SL>
+__global__ void __launch_bounds__(BLOCK) k_redo(SceneView sv, RenderArgs a, uint2* __restrict__ list, uint32_t cap,
+                                                float4* __restrict__ sbuf, uint32_t sb_ss, uint32_t sb_sp,
+                                                uint32_t* __restrict__ ovf, unsigned long long* __restrict__ counters)
+{
+    __shared__ uint32_t s_stack[SL * BLOCK];
+    __shared__ float s_light[kMaxDepth * BLOCK];
+    __shared__ uint4 s_top[kTopNodes * 4];
+    const int64_t gtid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    TravStack<BLOCK, SL> st{&s_stack[threadIdx.x], ovf + gtid * (kStackTotal - SL)};
+    const uint32_t ntop = (uint32_t)min(kTopNodes, sv.n_nodes4);
+    const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
+    for (uint32_t i = threadIdx.x; i < ntop * 4; i += BLOCK) s_top[i] = g[i];
+    __syncthreads();
+    st.top = (const lds_u4*)s_top;
+    st.ntop = ntop;
+    const uint32_t n = (uint32_t)min(counters[kRedoCounter], (unsigned long long)cap);
+    uint32_t rays_e = 0, rays_s = 0;
+    for (uint32_t i = (uint32_t)gtid; i < n; i += gridDim.x * BLOCK) {
+        const uint2 e = list[i];
+        if (e.x >= kRedoDone) continue;
+        redo_sample<BLOCK, SL>(sv, a, e.x, e.y, sbuf, sb_ss, sb_sp, rays_e, rays_s, st, &s_light[threadIdx.x]);
+    }
+    const uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
+    if (lane_id() == 0 && re + rs) {
+        atomicAdd(&counters[0], (unsigned long long)(re + rs));
+        atomicAdd(&counters[3], (unsigned long long)re);
+    }
 }
 
 template <bool ROW, bool COUNT, int BLOCK, int SL>
@@ -483,7 +568,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                 if (ANY) {
                     if (ts.best >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
                 } else {
-                    settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
+                    settle_closest<BLOCK, SL, TOPC, false, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
                     s.hid[p] = ts.best;
                     s.hit[P + p] = ts.bu;
                     s.hit[2 * P + p] = ts.bv;
@@ -728,6 +813,15 @@ struct PathCtl {
     int rs_noshadow;
     const uint32_t* __restrict__ uslot;
     RsStream rss;  // SAMP 4
+    // Deferred ties (SAMP 1, k_path DEFER): the main loop carries no octree
+    // walk; a sample whose closest-hit query ends on a flagged tie is dropped
+    // and (pixel, sample) appended to redo (counters[kRedoCounter] counts them,
+    // redo_cap entries are kept, kRedoEmpty until written).  Waves past the
+    // main loop trace the listed samples again, ties settled (redo_sample);
+    // k_redo takes any they leave.
+    uint2* __restrict__ redo;
+    uint32_t redo_cap;
+    uint32_t redo_inline;  // 0 (test hook, option redo_inline): no redo phase, k_redo takes every entry
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -898,7 +992,7 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
 
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int OCC = 1, int TAIL = 0, int PROF = 0,
-          int HELP = 0, int SAMP = 0, bool SOA = false>
+          int HELP = 0, int SAMP = 0, bool SOA = false, bool DEFER = false>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
@@ -1195,19 +1289,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 ps_t = stamp();
                 ps_fetch += ps_t - pt_t;
             }
-            {  // finished closest hits: the triangle index, ties answered by the octree
-                // (settle_closest, split so the rare octree walk sits behind a wave-uniform skip)
-                const bool fin = has_pix && !in_query && !cam && !qany;
-#ifdef TMPT_EXP_NOSETTLE  // cost experiment: no octree re-answer
-                if (fin) ts.best >>= 1;
-#else
-                const bool tie = fin && octree_tie(sv, ts);
-                if (wany(tie)) {
-                    if (tie) settle_closest(sv, r.o, r.d, kMinT, kMaxT, ts);
-                }
-                if (fin && !tie) ts.best >>= 1;
-#endif
-            }
             // ---- finished queries: shade
             bool finish = false, want_off = false;
             f3 color = mk(0.0f, 0.0f, 0.0f);
@@ -1216,6 +1297,41 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     finish = true;
                     if (depth < (uint32_t)kMaxDepth) color = sky(r.d);
                 } else if (!qany) {  // closest hit (Trace, main.cpp:91-109)
+                    // the triangle index; a tie is answered again by the octree
+                    // (settle_closest, split so the rare walk sits behind a wave-
+                    // uniform skip).  Only here: a lane reaches this branch once
+                    // per query (a HELP lane waiting on shadow answers does not).
+#ifdef TMPT_EXP_NOSETTLE  // cost experiment: no octree re-answer
+                    ts.best >>= 1;
+#else
+                    bool drop = false;
+                    if (DEFER) {
+                        // the deferring kernel: a tied sample is dropped here
+                        // (its rays so far uncounted: depth + 1 closest-hit
+                        // queries and one shadow query per earlier hit) and
+                        // traced again whole by redo_sample.  It finishes at
+                        // once with colour x = -1 (no path colour is negative),
+                        // which the colour-buffer stores below skip.
+                        drop = octree_tie(sv, ts);
+                        if (TMPT_RARE(wany(drop))) {
+                            if (drop) {
+                                const unsigned long long slot = atomicAdd(&counters[kRedoCounter], 1ull);
+                                if (slot < (unsigned long long)pc.redo_cap) pc.redo[slot] = make_uint2(pix, smp);
+                                rays_e -= depth + 1u;
+                                rays_s -= depth;
+                                depth = 0;
+                                ts.best = -1;
+                            }
+                        }
+                        ts.best >>= 1;  // -1 stays -1
+                    } else {
+                    const bool tie = octree_tie(sv, ts);
+                    if (TMPT_RARE(wany(tie))) {
+                        if (tie) settle_closest<BLOCK, SL, true, SOA, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
+                    }
+                    if (!tie) ts.best >>= 1;
+                    }
+#endif
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
                         // the hit record's loads go out first; RandomUnitVector
                         // (RNG + sincos, independent of them) runs while they are
@@ -1256,6 +1372,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         }
                     } else {
                         color = sky(r.d);  // main.cpp:106-107
+                        if (DEFER && drop) color.x = -1.0f;
                         finish = true;
                     }
                 } else if (SAMP < 3) {  // shadow query of bounce depth-1
@@ -1352,8 +1469,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
 #endif
                             col = color;
                         } else {
-                            if (pc.pair && odd) __builtin_nontemporal_store((f32x4){col.x, col.y, col.z, 0.0f}, dst - 1);
-                            __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f}, dst);
+                            // DEFER: a dropped sample's slot (x = -1) is redo_sample's
+                            if (pc.pair && odd && (!DEFER || !(col.x < 0.0f)))
+                                __builtin_nontemporal_store((f32x4){col.x, col.y, col.z, 0.0f}, dst - 1);
+                            if (!DEFER || !(color.x < 0.0f))
+                                __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f}, dst);
                         }
                     } else
                         col = col + color;
@@ -1412,7 +1532,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
 #ifndef TMPT_EXP_NOROOT  // cost experiment: no root box test
-                if (a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
+                if (!DEFER && TMPT_RARE(a.root_check) && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
                     in_query = false;  // a camera ray outside the reference's root box: a counted miss
                     atomicAdd(&sv.oct->ties[1], 1ull);
                 }
@@ -1481,15 +1601,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const bool stepping = in_query && ((ts.node < 0) == leaf_round);
                 bool done = false;
                 if (leaf_round) {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2, SOA>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2, SOA, false, DEFER>(sv, r, qany, ts, st, cnt);
                 } else {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1, SOA>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1, SOA, false, DEFER>(sv, r, qany, ts, st, cnt);
                 }
                 if (done) in_query = false;
                 if (stepping && ((kFull && pc.cost_out) || dp0 > 0.0f)) ++psteps;
             } else if (in_query && (ts.node < 0) == leaf_round) {
                 TravCount c1;
-                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true, 0, SOA>(sv, r, qany, ts, st, c1)) in_query = false;
+                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true, 0, SOA, false, DEFER>(sv, r, qany, ts, st, c1)) in_query = false;
                 TravCount& dst = qany ? cnt_s : cnt;
                 dst.nodes += c1.nodes;
                 dst.tris += c1.tris;
@@ -1500,6 +1620,54 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 (leaf_round ? pt_leaf : pt_node) += t - pt_t;
                 pt_t = t;
             }
+        }
+    }
+    if (DEFER && pc.redo_inline) {
+        // Redo phase: the wave's main loop is over; it traces the samples the
+        // main loops dropped on ties (one per lane, by ticket), while the other
+        // waves finish theirs, so the re-traces fill the frame's tail.  A lane
+        // waits on an entry only while some wave is still in its main loop (the
+        // list is final once every wave is past it); a wave that sees nothing
+        // change for kRedoPatience leaves its tickets to k_redo.
+        constexpr uint64_t kRedoPatience = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
+        const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
+        uint32_t t = 0;
+        if (lane_id() == 0) {
+            atomicAdd(&counters[kRedoWaves], 1ull);
+            t = (uint32_t)atomicAdd(&counters[kRedoTaken], 64ull);
+        }
+        t = (uint32_t)__shfl((int)t, 0) + lane_id();
+        unsigned long long seen = ~0ull;
+        uint64_t since = 0;
+        for (;;) {
+            const unsigned long long listed =
+                __hip_atomic_load(&counters[kRedoCounter], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t lim = (uint32_t)min(listed, (unsigned long long)pc.redo_cap);
+            uint2 e = make_uint2(kRedoEmpty, 0u);
+            if (t < lim) e = redo_load(pc.redo + t);
+            const bool have = e.x < kRedoDone;
+            if (wany(have)) {
+                if (have) {
+                    redo_sample<BLOCK, SL>(sv, a, e.x, e.y, pc.sbuf, pc.sb_ss, pc.sb_sp, rays_e, rays_s, st, light);
+                    redo_mark(pc.redo + t);
+                    atomicAdd(&counters[kRedoTraced], 1ull);
+                    t = (uint32_t)atomicAdd(&counters[kRedoTaken], 1ull);
+                }
+                since = 0;
+                continue;
+            }
+            const unsigned long long past =
+                __hip_atomic_load(&counters[kRedoWaves], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (past >= waves && !wany(t < lim)) break;
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long sig = (past << 40) ^ listed;
+            if (sig != seen || since == 0) {
+                seen = sig;
+                since = now;
+            } else if (now - since > kRedoPatience) {
+                break;
+            }
+            __builtin_amdgcn_s_sleep(16);
         }
     }
     if (SAMP == 4 && lane_id() == 0) {
@@ -2450,13 +2618,86 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         return 0;
     };
     if (!ordered) {
-        if (final_launch(as)) return -1;
+        // Deferred ties (PathCtl::redo, k_path DEFER): with per-sample colours
+        // (sbuf) a tied sample can be traced again on its own, so the main loop
+        // runs without the octree walk and root-box test (and takes the first
+        // triangle met on a tie, flagged) and the launch's waves trace the
+        // dropped samples in their tail (k_redo the rest).  Only when no camera
+        // ray needs the root-box test (root_check = 0).  Auto: at >= 192 samples
+        // per resident lane, where the tail hides the re-traces -- bench frame,
+        // k_path ms, base (no octree) / ties settled inline / deferred: N=1
+        // 184.8 / 190.2 / 185.3, 1/2 93.1 / 96.3 / 94.9, 1/4 47.7 / 49.4 /
+        // 49.8, 1/8 24.6 / 25.5 / 27.1
+        const bool defer = a.jt && !count && !prof && !soa && pc.sbuf && a.root_check == 0 && o.tie_defer != 0 &&
+                           (o.tie_defer > 0 || a.slots * (int64_t)a.spp >= 192 * lanes);
+        bool redo = defer && s.oct_view && o.tie_rule == 0;
+        if (redo && o.redo_cap > 0 && s.redo_cap != (uint32_t)o.redo_cap) {  // the test hook's size
+            (void)hipFree(s.redo);
+            s.redo = nullptr;
+            s.redo_cap = 0;
+        }
+        if (redo && s.redo_cap == 0) {
+            int64_t cap = std::min<int64_t>(1ll << 31, std::max<int64_t>(1 << 16, a.slots * (int64_t)a.spp / 128));
+            if (o.redo_cap > 0) cap = o.redo_cap;
+            if (hipMalloc(&s.redo, sizeof(uint2) * (size_t)cap) == hipSuccess) s.redo_cap = (uint32_t)cap;
+            else (void)hipGetLastError();
+        }
+        if (redo && s.redo_cap == 0) redo = false;
+        // (the deferring kernel keeps the first triangle met on a tie and flags
+        // it: only the redo pass gives those samples their answer)
+        PathFn fn_main = fn;
+        if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, true>;
+        s.path_launches = 1;
+        for (int attempt = 0;; ++attempt) {
+            pc.redo = redo ? s.redo : nullptr;
+            pc.redo_cap = redo ? s.redo_cap : 0u;
+            pc.redo_inline = o.redo_inline ? 1u : 0u;
+            if (redo) TMPT_HIP(hipMemsetAsync(s.redo, 0xFF, sizeof(uint2) * (size_t)s.redo_cap, s.stream));
+            TMPT_HIP(hipEventRecord(s.path_ev[2], s.stream));
+            fn_main<<<grid, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, (uint32_t*)s.ws, d_counters);
+            TMPT_HIP(hipGetLastError());
+            TMPT_HIP(hipEventRecord(s.path_ev[3], s.stream));
+            if (!redo) break;
+            // the list's count and the entries the launch traced itself
+            TMPT_HIP(hipMemcpyAsync(s.counters_host + kRedoCounter, d_counters + kRedoCounter,
+                                    4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s.stream));
+            TMPT_HIP(hipStreamSynchronize(s.stream));
+            const unsigned long long n = s.counters_host[kRedoCounter];
+            const unsigned long long traced = s.counters_host[kRedoTraced];
+            s.redo_samples = (int64_t)n;
+            if (n > s.redo_cap && attempt == 0) {
+                // the list overflowed: grow it to the count (the same frame lists
+                // the same samples) or, failing that, render with the exact kernel
+                (void)hipFree(s.redo);
+                s.redo = nullptr;
+                s.redo_cap = 0;
+                if (n < (1ull << 31) && hipMalloc(&s.redo, sizeof(uint2) * (size_t)n) == hipSuccess) {
+                    s.redo_cap = (uint32_t)n;
+                } else {
+                    (void)hipGetLastError();
+                    redo = false;
+                    fn_main = fn;
+                    s.redo_samples = 0;
+                }
+                TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
+                TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
+                continue;
+            }
+            if (traced < std::min<unsigned long long>(n, s.redo_cap)) {  // entries the launch left
+                TMPT_HIP(hipEventRecord(s.path_ev[0], s.stream));
+                k_redo<kBlk, kPathSL><<<grid, kBlk, 0, s.stream>>>(view(s), as, s.redo, s.redo_cap, pc.sbuf, pc.sb_ss,
+                                                                  pc.sb_sp, (uint32_t*)s.ws, d_counters);
+                TMPT_HIP(hipGetLastError());
+                TMPT_HIP(hipEventRecord(s.path_ev[1], s.stream));
+                s.path_launches = 2;
+            }
+            break;
+        }
         if (pc.sbuf) {
             k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(pc.sbuf, a.slots, a.spp,
                                                                              a.spp_recip, d_out);
             TMPT_HIP(hipGetLastError());
         }
-        s.path_launches = 1;
         return 0;
     }
     uint32_t* base = heads + head_words;
@@ -3231,6 +3472,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.row_engine = 0;
     s.stream_fallbacks = 0;
     s.chain_pixels = 0;
+    s.redo_samples = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
@@ -3267,6 +3509,17 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.render_ms = ms;
     s.tie_queries = c[kTieCounter];
     s.root_misses = c[kTieCounter + 1];
+#ifdef TMPT_EXP_WALKSTAT
+    {
+        unsigned long long w[4] = {0, 0, 0, 0};
+        if (hipMemcpyFromSymbol(w, HIP_SYMBOL(g_walkstat), sizeof(w)) == hipSuccess && w[3]) {
+            fprintf(stderr, "octree walks %llu: nodes %.1f, triangles %.1f per walk, max nodes %llu\n", w[3],
+                    (double)w[0] / w[3], (double)w[1] / w[3], w[2]);
+            const unsigned long long z[4] = {0, 0, 0, 0};
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_walkstat), z, sizeof(z));
+        }
+    }
+#endif
     if (progressive) s.prog_key[6] = a.smp_end < a.spp ? a.smp_end : -1;
     if (persistent) {  // one kernel for both query kinds
         // k_path launches only (the render's other kernels: order keys, sort,

@@ -187,7 +187,8 @@ __device__ __forceinline__ void trav_init(TravState& ts, float tmax)
 // per-ray ranges): the far-distance slack is applied by magnitude, so it
 // widens a box's interval for negative distances too (kTfarSlack alone would
 // shrink it there); the path engines' range kMinT..kMaxT never needs it.
-template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0, bool SOA = false, bool NEG = false>
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false, int KIND = 0, bool SOA = false, bool NEG = false,
+          bool FLAG = false>
 __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const TravRay& r, bool any,
                                                    TravState& ts, TravStack<BLOCK, SL>& st,
                                                    TravCount& cnt, float tlo = 0.0f, float tmin = kMinT,
@@ -285,8 +286,10 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                 // id = 2 x index: comparing it with best (2 x index | tie bit)
                 // orders the indices; the tie bit never decides
                 const int id = __float_as_int(c.y);
-                const bool tie = t == ts.bt && ts.best >= 0;
-                if (t < ts.bt || (tie && id < ts.best)) {
+                // (no triangle is accepted at t == tmax, the initial bt: the
+                // flag it sets on best = -1 leaves -1)
+                const bool tie = t == ts.bt;
+                if (t < ts.bt || (!FLAG && tie && id < ts.best)) {
                     ts.bt = t;
                     ts.bu = u;
                     ts.bv = v;
@@ -346,14 +349,16 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             (void)tie0;
             (void)tie1;
 #else
-            const bool tie0 = ok0 && t0 == ts.bt && ts.best >= 0;
-            const bool acc0 = ok0 && (t0 < ts.bt || (tie0 && id0 < ts.best));
+            // FLAG: the first triangle met keeps a tie (the flag sends the query
+            // to be answered again); otherwise the lower index takes it
+            const bool tie0 = ok0 && t0 == ts.bt;
+            const bool acc0 = ok0 && (t0 < ts.bt || (!FLAG && tie0 && id0 < ts.best));
             ts.bt = acc0 ? t0 : ts.bt;
             ts.bu = acc0 ? u0 : ts.bu;
             ts.bv = acc0 ? w0 : ts.bv;
             ts.best = (acc0 ? id0 : ts.best) | (int)tie0;
-            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt && ts.best >= 0;
-            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (tie1 && id1 < ts.best));
+            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt;
+            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (!FLAG && tie1 && id1 < ts.best));
             ts.bt = acc1 ? t1 : ts.bt;
             ts.bu = acc1 ? u1 : ts.bu;
             ts.bv = acc1 ? w1 : ts.bv;
@@ -417,9 +422,20 @@ __device__ __forceinline__ f3 ref_inverse(f3 d) { return mk(1.0f / d.x, 1.0f / d
 // ray from outside the root box can fail it while hitting a triangle (one
 // that grazes the root's faces at the floor's corners, main.cpp:153-162 puts
 // them on the root's boundary).
+#ifdef TMPT_EXP_CALL
+#define TMPT_WALK_INLINE __noinline__
+#else
+#define TMPT_WALK_INLINE __forceinline__
+#endif
+
+__device__ TMPT_WALK_INLINE bool root_slab(const OctNode* __restrict__ nodes, f3 o, f3 d, float tmin, float tmax)
+{
+    return ref_slab(o, ref_inverse(d), nodes[0].lo, nodes[0].hi, tmin, tmax);
+}
+
 __device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax)
 {
-    return ref_slab(o, ref_inverse(d), sv.oct->nodes[0].lo, sv.oct->nodes[0].hi, tmin, tmax);
+    return root_slab(sv.oct->nodes, o, d, tmin, tmax);
 }
 
 // HitSceneInternal (scene.cpp:21-52) over the preorder octree: a node whose
@@ -431,16 +447,26 @@ __device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d,
 // maths.cpp:341-342 forms them.  `target`: the closest t over all triangles
 // (the BVH's answer): no triangle has a smaller one, so the first met at
 // exactly `target` is the reference's answer and the walk stops there.
-__device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float target,
-                                           float& bt, float& bu, float& bv)
+// The walk itself takes plain pointers and returns by value, so it can be
+// built out of line (TMPT_EXP_CALL) without a stack frame for its results.
+struct OctHit {
+    int best;
+    float t, u, v;
+};
+
+__device__ TMPT_WALK_INLINE OctHit octree_walk(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
+                                               int n_oct, const TriOrig* __restrict__ tris, f3 o, f3 d,
+                                               float tmin, float tmax, float target)
 {
     const f3 inv = ref_inverse(d);
-    int best = -1;
-    float tb = tmax, ub = 0.0f, vb = 0.0f;
-    const OctNode* __restrict__ nodes = sv.oct->nodes;
-    const int32_t* __restrict__ refs = sv.oct->refs;
-    const int n_oct = sv.oct->n;
+    OctHit h{-1, tmax, 0.0f, 0.0f};
+#ifdef TMPT_EXP_WALKSTAT  // cost experiment: nodes and triangles a walk visits
+    uint32_t wn = 0, wt = 0;
+#endif
     for (int i = 0; i < n_oct;) {
+#ifdef TMPT_EXP_WALKSTAT
+        ++wn;
+#endif
         const float4 lo = nodes[i].lo, hi = nodes[i].hi;
         if (!ref_slab(o, inv, lo, hi, tmin, tmax)) {
             i = __float_as_int(lo.w);
@@ -451,15 +477,15 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
             const int cnt = refs[ref];
             for (int k = 1; k <= cnt; ++k) {
                 const int id = refs[ref + k];
-                const float4* p = reinterpret_cast<const float4*>(sv.tri_orig + id);
+                const float4* p = reinterpret_cast<const float4*>(tris + id);
                 const float4 a = p[0], b = p[1], c = p[2];
                 const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
                 float t, u, v;
-                if (mt_test(o, d, v0, v1 - v0, v2 - v0, tmin, tmax, t, u, v) && t < tb) {
-                    tb = t;
-                    ub = u;
-                    vb = v;
-                    best = id;
+#ifdef TMPT_EXP_WALKSTAT
+                ++wt;
+#endif
+                if (mt_test(o, d, v0, v1 - v0, v2 - v0, tmin, tmax, t, u, v) && t < h.t) {
+                    h = OctHit{id, t, u, v};
                     if (t == target) {  // first at the minimum: nothing can replace it
                         i = n_oct;
                         break;
@@ -469,10 +495,24 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
         }
         ++i;  // a leaf's skip link is the next node; an inner node descends to child 0
     }
-    bt = tb;
-    bu = ub;
-    bv = vb;
-    return best;
+#ifdef TMPT_EXP_WALKSTAT
+    extern __device__ unsigned long long g_walkstat[4];
+    atomicAdd(&g_walkstat[0], (unsigned long long)wn);
+    atomicAdd(&g_walkstat[1], (unsigned long long)wt);
+    atomicMax(&g_walkstat[2], (unsigned long long)wn);
+    atomicAdd(&g_walkstat[3], 1ull);
+#endif
+    return h;
+}
+
+__device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float target,
+                                              float& bt, float& bu, float& bv)
+{
+    const OctHit h = octree_walk(sv.oct->nodes, sv.oct->refs, sv.oct->n, sv.tri_orig, o, d, tmin, tmax, target);
+    bt = h.t;
+    bu = h.u;
+    bv = h.v;
+    return h.best;
 }
 
 // Whether a finished closest-hit query is a flagged tie the octree answers.
@@ -484,13 +524,17 @@ __device__ __forceinline__ bool octree_tie(const SceneView& sv, const TravState&
 // A finished closest-hit query: the triangle index from TravState::best; a
 // flagged tie is answered again over the octree (the reference's pick among
 // the tied triangles, and its whole answer for that ray); without an octree
-// the lowest index stands.
-__device__ __forceinline__ void settle_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
-                                               TravState& ts)
+// the lowest index stands.  (The walk stops at the first triangle at the tied
+// t, which is the reference's answer: nothing lies nearer.)
+template <int BLOCK, int SL, bool TOPC, bool SOA, bool NEG>
+__device__ __forceinline__ void settle_closest(const SceneView& sv, const TravRay& r, float tlo, float tmin,
+                                               float tmax, TravState& ts, TravStack<BLOCK, SL>& st)
 {
+    (void)tlo;
+    (void)st;
     if (octree_tie(sv, ts)) {
         atomicAdd(&sv.oct->ties[0], 1ull);
-        ts.best = octree_closest(sv, o, d, tmin, tmax, ts.bt, ts.bt, ts.bu, ts.bv);
+        ts.best = octree_closest(sv, r.o, r.d, tmin, tmax, ts.bt, ts.bt, ts.bu, ts.bv);
     } else {
         ts.best >>= 1;  // -1 stays -1
     }
@@ -523,7 +567,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
         const float tlo = fminf(tmin, 0.0f);
         while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA, NEG>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
-        if (!ANY) settle_closest(sv, r.o, r.d, tmin, tmax, ts);
+        if (!ANY) settle_closest<BLOCK, SL, TOPC, SOA, NEG>(sv, r, tlo, tmin, tmax, ts, st);
         else ts.best >>= 1;  // the doubled index of the first accepted triangle (-1 stays -1)
     }
     bt = ts.bt;
