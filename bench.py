@@ -392,11 +392,12 @@ def main() -> None:
     ext_ms = sh_ms = 0.0
     ext_rays = sh_rays = 0
     ext_launches = 0
-    ties = roots = 0
+    ties = roots = redo = 0
     for _ in range(args.steps):
         r, st = step()
         ties += st.tie_queries
         roots += st.root_misses
+        redo += st.redo_samples
         rays += r
         ext_ms += st.extend_ms
         sh_ms += st.shadow_ms
@@ -457,6 +458,35 @@ def main() -> None:
                 compare[name].update({"row_engine": sorted({3: "streaming", 2: "iterated", 1: "lane per row"}
                                                            .get(e, str(e)) for e in engines),
                                       "stream_fallbacks": fallbacks})
+    # ---- the same frames with ties by the lowest index (option tie_rule=index,
+    # the exact-semantics contract of rounds 1-3): what the reference's own tie
+    # answer costs (reported, not `value`)
+    index_rule = None
+    if not args.no_compare and st0.tie_rule == 0:
+        scene.set_option("tie_rule", 1)
+        step()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        csteps = min(args.steps, 5)
+        crays = 0
+        for _ in range(csteps):
+            crays += step()[0]
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        cel = time.perf_counter() - t1
+        if dist_on:
+            t = torch.tensor([cel], dtype=torch.float64, device=gdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cel = float(t.item())
+            r = torch.tensor([crays], dtype=torch.int64, device=gdev)
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            crays = int(r.item())
+        scene.set_option("tie_rule", 0)
+        index_rule = {"value": round(crays / cel / 1e6, 2), "ms_per_step": round(cel / csteps * 1e3, 2),
+                      "steps": csteps, "cost_of_reference_ties": round(1.0 - value / (crays / cel / 1e6), 4)}
     if rank != 0:
         scene.close()
         dist.destroy_process_group()
@@ -564,7 +594,12 @@ def main() -> None:
         "reference_octree": {"nodes": st0.octree_nodes, "leaves": st0.octree_leaves, "refs": st0.octree_refs,
                              "build_ms": round(st0.octree_build_ms, 1), "tie_rule": "visit" if st0.tie_rule == 0 else "index",
                              "tie_queries_per_step": ties // max(args.steps, 1),
-                             "root_misses_per_step": roots // max(args.steps, 1)},
+                             "root_misses_per_step": roots // max(args.steps, 1),
+                             # sample seeding at >= 192 samples per lane: tied samples dropped by
+                             # the main loop and traced again in the launch's tail
+                             "tie_answer": "deferred" if redo else "in the main loop",
+                             "redo_samples_per_step": redo // max(args.steps, 1),
+                             "index_rule": index_rule},
     }
     print(json.dumps(out), flush=True)
     scene.close()

@@ -992,12 +992,20 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
 
 
 template <bool COUNT, int BLOCK, int SL, int STEPS, int SHADE_MIN, int OCC = 1, int TAIL = 0, int PROF = 0,
-          int HELP = 0, int SAMP = 0, bool SOA = false, bool DEFER = false>
+          int HELP = 0, int SAMP = 0, bool SOA = false, int TIES = 0>
 __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a, PathCtl pc,
                                                 uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ ovf,
                                                 unsigned long long* __restrict__ counters)
 {
+    // TIES: how closest hits tied on t are answered.  0: the leaf keeps the
+    // lowest index beside the tie flag and a flagged query is re-answered over
+    // the octree when there is one (else the lowest index stands); 2: the
+    // octree is there (the caller guarantees it), so the leaf keeps the first
+    // triangle met and only flags the tie, and the octree answers; 1 (DEFER,
+    // sample seeding): as 2, but a flagged sample is dropped and traced again
+    // in the redo phase -- the main loop carries no octree walk.
+    constexpr bool DEFER = TIES == 1, FLAG = TIES != 0;
     __shared__ uint32_t s_stack[SL * BLOCK];
     // SAMP 3, 4 (shadow-free speculation): no light terms, no pending next ray
     __shared__ float s_light[SAMP >= 3 ? 1 : kMaxDepth * BLOCK];
@@ -1601,15 +1609,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 const bool stepping = in_query && ((ts.node < 0) == leaf_round);
                 bool done = false;
                 if (leaf_round) {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2, SOA, false, DEFER>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 2, SOA, false, FLAG>(sv, r, qany, ts, st, cnt);
                 } else {
-                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1, SOA, false, DEFER>(sv, r, qany, ts, st, cnt);
+                    if (stepping) done = trav_step4q2_mixed<false, BLOCK, SL, true, 1, SOA, false, FLAG>(sv, r, qany, ts, st, cnt);
                 }
                 if (done) in_query = false;
                 if (stepping && ((kFull && pc.cost_out) || dp0 > 0.0f)) ++psteps;
             } else if (in_query && (ts.node < 0) == leaf_round) {
                 TravCount c1;
-                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true, 0, SOA, false, DEFER>(sv, r, qany, ts, st, c1)) in_query = false;
+                if (trav_step4q2_mixed<COUNT, BLOCK, SL, true, 0, SOA, false, FLAG>(sv, r, qany, ts, st, c1)) in_query = false;
                 TravCount& dst = qany ? cnt_s : cnt;
                 dst.nodes += c1.nodes;
                 dst.tris += c1.tris;
@@ -2645,8 +2653,11 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         if (redo && s.redo_cap == 0) redo = false;
         // (the deferring kernel keeps the first triangle met on a tie and flags
         // it: only the redo pass gives those samples their answer)
+        // (with the octree but no deferral: the leaf only flags ties, TIES 2)
         PathFn fn_main = fn;
-        if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, true>;
+        if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
+        else if (fn == fn_default && a.jt && !count && !soa && s.oct_view && o.tie_rule == 0)
+            fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
         s.path_launches = 1;
         for (int attempt = 0;; ++attempt) {
             pc.redo = redo ? s.redo : nullptr;
@@ -2676,7 +2687,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                 } else {
                     (void)hipGetLastError();
                     redo = false;
-                    fn_main = fn;
+                    fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
                     s.redo_samples = 0;
                 }
                 TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
