@@ -2566,6 +2566,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
     if (o.pair >= 0) pair = o.pair;
     if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
+    // pixel seeding with the octree there: the leaves only flag ties (TIES 2)
+    if (!a.jt && !count && !prof && s.oct_view && o.tie_rule == 0)
+        fn = help ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>
+                  : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>;
     const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
