@@ -223,6 +223,7 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    walk) and traced again, ties settled, by the launch's waves once
  *                    their main loop is done (-1 = auto, 0 = off: ties settled in the
  *                    main loop, 1 = on); the image and ray counts are the same either way
+ *   redo_lanes       tie_defer: lanes per wave that take the re-traces (1..64, default 4)
  *   redo_cap         test hook (0 = auto): the capacity of tie_defer's sample list; a
  *                    frame that overflows it is rendered again with the list grown
  *   redo_inline      test hook (1): 0 leaves every dropped sample to the second launch

@@ -52,7 +52,7 @@ with tm.Scene(tris[:1]) as _probe:  # render-option defaults, restored after eac
     DEFAULTS = {}
     for _k in ("sample_block", "sbuf_max", "sbuf_pair", "pilot", "help", "pair", "balance", "dprio", "wave_cap", "pixel_chains", "rowspec",
                "rowspec_wmax", "rowspec_windows", "rowspec_spread", "rowspec_groups", "rowspec_noshadow",
-               "rowspec_chase", "rowspec_stream", "wf_bins", "tie_rule", "tie_defer", "redo_cap", "redo_inline"):
+               "rowspec_chase", "rowspec_stream", "wf_bins", "tie_rule", "tie_defer", "redo_cap", "redo_inline", "redo_lanes"):
         try:  # an older library build (TMPT_LIB_PATH) may not know every option
             DEFAULTS[_k] = _probe.get_option(_k)
         except tm.TmptError:

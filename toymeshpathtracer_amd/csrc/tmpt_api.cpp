@@ -123,6 +123,7 @@ const OptionDef kOptions[] = {
     {"tie_defer", false, -1, 1, &Options::tie_defer, nullptr, nullptr},
     {"redo_cap", false, 0, 1 << 30, &Options::redo_cap, nullptr, nullptr},
     {"redo_inline", false, 0, 1, &Options::redo_inline, nullptr, nullptr},
+    {"redo_lanes", false, 1, 64, &Options::redo_lanes, nullptr, nullptr},
     {"rowspec", false, 0, 1, &Options::rowspec, nullptr, nullptr},
     {"rowspec_wmax", false, 0, 16384, &Options::rowspec_wmax, nullptr, nullptr},
     {"rowspec_windows", false, 0, 32, &Options::rowspec_windows, nullptr, nullptr},

@@ -164,6 +164,7 @@ struct Options {
                               // main kernel carries no octree walk (-1 auto, 0 off, 1 on)
     int redo_cap = 0;         // test hook: the redo list's capacity in entries (0 = auto; a small one
                               // overflows, and the frame is rendered again with the list grown)
+    int redo_lanes = 4;       // tie_defer: lanes per wave that take re-traces in the launch's tail
     int redo_inline = 1;      // test hook: 0 = the deferring kernel's waves leave every dropped sample
                               // to the k_redo launch (its fallback) instead of tracing them in their tail
 };

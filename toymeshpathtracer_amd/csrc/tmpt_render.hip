@@ -822,6 +822,7 @@ struct PathCtl {
     uint2* __restrict__ redo;
     uint32_t redo_cap;
     uint32_t redo_inline;  // 0 (test hook, option redo_inline): no redo phase, k_redo takes every entry
+    uint32_t redo_lanes;   // lanes per wave that take redo tickets (1..64)
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -1639,12 +1640,17 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         // change for kRedoPatience leaves its tickets to k_redo.
         constexpr uint64_t kRedoPatience = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
         const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
+        // pc.redo_lanes lanes of the wave take tickets: a re-trace is one
+        // lane's whole path, so fewer per wave spread them over more waves
+        // (the wave waits for its slowest lane).  Bench frame, k_path ms with
+        // 64 / 16 / 4 / 1 lanes: 1/8 shard 27.3 / 26.4 / 26.1 / 25.8, N=1
+        // 184.8 / 184.9 / 184.5 (profiles/r04_ties/redo_lanes_*.log): 4
         uint32_t t = 0;
         if (lane_id() == 0) {
             atomicAdd(&counters[kRedoWaves], 1ull);
-            t = (uint32_t)atomicAdd(&counters[kRedoTaken], 64ull);
+            t = (uint32_t)atomicAdd(&counters[kRedoTaken], (unsigned long long)pc.redo_lanes);
         }
-        t = (uint32_t)__shfl((int)t, 0) + lane_id();
+        t = lane_id() < pc.redo_lanes ? (uint32_t)__shfl((int)t, 0) + lane_id() : 0xFFFFFFFFu;
         unsigned long long seen = ~0ull;
         uint64_t since = 0;
         for (;;) {
@@ -2667,6 +2673,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             pc.redo = redo ? s.redo : nullptr;
             pc.redo_cap = redo ? s.redo_cap : 0u;
             pc.redo_inline = o.redo_inline ? 1u : 0u;
+            pc.redo_lanes = (uint32_t)std::max(1, std::min(64, o.redo_lanes));
             if (redo) TMPT_HIP(hipMemsetAsync(s.redo, 0xFF, sizeof(uint2) * (size_t)s.redo_cap, s.stream));
             TMPT_HIP(hipEventRecord(s.path_ev[2], s.stream));
             fn_main<<<grid, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, (uint32_t*)s.ws, d_counters);
