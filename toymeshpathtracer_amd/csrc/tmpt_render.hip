@@ -195,6 +195,79 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
 __device__ unsigned long long g_walkstat[4];
 #endif
 
+// ============================================================ octree walk, one wave
+__device__ __forceinline__ float rlane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ int rlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// octree_walk (tmpt_traverse.h) for ONE query, run by the whole wave (every
+// lane active, every argument wave-uniform): the lanes test the slab of 64
+// consecutive preorder nodes at once and the DFS then steps through that
+// window on scalar masks (a failed node jumps to its skip link, a passed one
+// to the next node), so a window costs one memory round trip instead of one
+// per node; a visited leaf's triangles are tested one per lane, and the leaf
+// keeps what the serial scan would: the first triangle at the leaf's least t
+// when that t beats the best so far (strict <, scene.cpp:34).  The walk
+// stops at the first triangle at `target` (nothing is nearer).  The
+// reference visits ~100 nodes per tied query on the bench frame (up to ~950:
+// tools/ diag TMPT_EXP_WALKSTAT, profiles/r04_ties/walkstat_n1.log).
+__device__ __forceinline__ OctHit octree_walk_wave(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
+                                                   int n_oct, const TriOrig* __restrict__ tris, f3 o, f3 d,
+                                                   float tmin, float tmax, float target)
+{
+    const f3 inv = ref_inverse(d);
+    const int lane = lane_id();
+    OctHit h{-1, tmax, 0.0f, 0.0f};
+    int i = 0;
+    while (i < n_oct) {
+        const int j = i + lane;
+        bool pass = false;
+        int skip = 0, ref = -1;
+        if (j < n_oct) {
+            const float4 lo = nodes[j].lo, hi = nodes[j].hi;
+            pass = ref_slab(o, inv, lo, hi, tmin, tmax);
+            skip = __float_as_int(lo.w);
+            ref = __float_as_int(hi.w);
+        }
+        const uint64_t P = wballot(pass), L = wballot(pass && ref >= 0);
+        int cur = i;
+        const int end = min(i + 64, n_oct);
+        while (cur < end) {
+            const int k = cur - i;
+            if (((P >> k) & 1ull) == 0) {
+                cur = rlane(skip, k);
+                continue;
+            }
+            if ((L >> k) & 1ull) {
+                const int r = rlane(ref, k);
+                const int cnt = refs[r];
+                for (int b = 0; b < cnt; b += 64) {
+                    float t = INFINITY, u = 0.0f, v = 0.0f;
+                    int id = -1;
+                    bool ok = false;
+                    if (b + lane < cnt) {
+                        id = refs[r + 1 + b + lane];
+                        const float4* p = reinterpret_cast<const float4*>(tris + id);
+                        const float4 a = p[0], bb = p[1], c = p[2];
+                        const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, bb.x, bb.y), v2 = mk(bb.z, bb.w, c.x);
+                        ok = mt_test(o, d, v0, v1 - v0, v2 - v0, tmin, tmax, t, u, v);
+                    }
+                    float m = ok ? t : INFINITY;
+                    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+                    const float mt = rlane(m, 0);
+                    if (mt < h.t) {
+                        const int f = (int)__builtin_ctzll(wballot(ok && t == mt));
+                        h = OctHit{rlane(id, f), mt, rlane(u, f), rlane(v, f)};
+                        if (mt == target) return h;
+                    }
+                }
+            }
+            ++cur;  // a leaf's skip link is the next node; an inner node descends to child 0
+        }
+        i = cur;
+    }
+    return h;
+}
+
 // ============================================================ deferred ties
 // A sample the deferring sample kernel (k_path DEFER) dropped on a tied
 // closest hit, traced again whole by one lane with ties settled
@@ -1298,6 +1371,34 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 ps_t = stamp();
                 ps_fetch += ps_t - pt_t;
             }
+            // Finished closest hits flagged as ties (not DEFER): each answered
+            // over the octree by the whole wave (octree_walk_wave), one after
+            // another -- here, where every lane is active.  A HELP lane
+            // waiting on shadow answers holds no fresh query.
+            bool settled = false;
+            if (!DEFER) {
+                const bool fin = has_pix && !in_query && !cam && !qany && !(HELP && waiting);
+                uint64_t T = wballot(fin && octree_tie(sv, ts));
+                if (TMPT_RARE(T != 0)) {
+                    const OctView* ov = sv.oct;
+                    do {
+                        const int l = (int)__builtin_ctzll(T);
+                        T &= T - 1;
+                        const f3 qo = mk(rlane(r.o.x, l), rlane(r.o.y, l), rlane(r.o.z, l));
+                        const f3 qd = mk(rlane(r.d.x, l), rlane(r.d.y, l), rlane(r.d.z, l));
+                        const OctHit h = octree_walk_wave(ov->nodes, ov->refs, ov->n, sv.tri_orig, qo, qd, kMinT, kMaxT,
+                                                          rlane(ts.bt, l));
+                        if (lane_id() == l) {
+                            atomicAdd(&ov->ties[0], 1ull);
+                            ts.best = h.best;
+                            ts.bt = h.t;
+                            ts.bu = h.u;
+                            ts.bv = h.v;
+                            settled = true;
+                        }
+                    } while (T != 0);
+                }
+            }
             // ---- finished queries: shade
             bool finish = false, want_off = false;
             f3 color = mk(0.0f, 0.0f, 0.0f);
@@ -1306,10 +1407,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     finish = true;
                     if (depth < (uint32_t)kMaxDepth) color = sky(r.d);
                 } else if (!qany) {  // closest hit (Trace, main.cpp:91-109)
-                    // the triangle index; a tie is answered again by the octree
-                    // (settle_closest, split so the rare walk sits behind a wave-
-                    // uniform skip).  Only here: a lane reaches this branch once
-                    // per query (a HELP lane waiting on shadow answers does not).
+                    // the triangle index (2 x index | tie flag in the leaves'
+                    // records); a tie was answered over the octree at the top of
+                    // the round, or (DEFER) drops the sample here
 #ifdef TMPT_EXP_NOSETTLE  // cost experiment: no octree re-answer
                     ts.best >>= 1;
 #else
@@ -1333,12 +1433,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             }
                         }
                         ts.best >>= 1;  // -1 stays -1
-                    } else {
-                    const bool tie = octree_tie(sv, ts);
-                    if (TMPT_RARE(wany(tie))) {
-                        if (tie) settle_closest<BLOCK, SL, true, SOA, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
-                    }
-                    if (!tie) ts.best >>= 1;
+                    } else if (!settled) {
+                        ts.best >>= 1;  // the index (a tie was answered above)
                     }
 #endif
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
