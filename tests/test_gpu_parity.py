@@ -995,6 +995,31 @@ def test_octree_rule_every_engine(gpu, engine, seed, oseed):
     sc.close()
 
 
+@pytest.mark.parametrize("seed,oseed", [(tm.SEED_PIXEL, oracle.SEED_PIXEL), (tm.SEED_SAMPLE, oracle.SEED_SAMPLE)])
+def test_octree_many_way_ties(gpu, seed, oseed):
+    """Every hit a many-way tie: suzanne's triangles 12 times over (the floor
+    once), so each closest hit on the mesh is tied between >= 12 identical
+    triangles, the octree (10 M references) bottoms out at depth 10 with
+    leaves of dozens of references, and every tied query walks it (k_path's
+    wave walk, 64 nodes / triangles per round trip; the batched HitScene's
+    serial walk).  The frame and the batched answers equal the oracle's
+    octree in its visit order (scene.cpp:21-52: the first copy met wins)."""
+    tris, bmin, bmax = tm.load_scene(data("suzanne.obj"))
+    reps = (12,) + (1,) * (tris.ndim - 1)
+    many = np.ascontiguousarray(np.concatenate([np.tile(tris[:-2], reps), tris[-2:]]))
+    w, h, spp = 96, 64, 2
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    osc = _ref_oracle(many, bmin, bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oseed)
+    with tm.Scene(many, bounds=(bmin, bmax)) as sc:
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=seed)
+        assert sc.stats().tie_queries > 0
+        rays_in = _random_rays(many, 4000, seed=11)
+        ids, hits = sc.hit_scene_batch(rays_in, 0.001, 1.0e7)
+    assert rays == ref_rays and np.array_equal(img, ref)
+    _same_answers(ids, hits, *osc.hit_batch(rays_in, 0.001, 1.0e7))
+
+
 def test_octree_render_multi_and_rebuild(gpu):
     """tmpt_render_multi with the octree box builds it on every device's scene
     (the frame equals the oracle octree's); building the octree again on a
