@@ -392,12 +392,13 @@ def main() -> None:
     ext_ms = sh_ms = 0.0
     ext_rays = sh_rays = 0
     ext_launches = 0
-    ties = roots = redo = 0
+    ties = roots = redo = redo_late = 0
     for _ in range(args.steps):
         r, st = step()
         ties += st.tie_queries
         roots += st.root_misses
         redo += st.redo_samples
+        redo_late += st.redo_late
         rays += r
         ext_ms += st.extend_ms
         sh_ms += st.shadow_ms
@@ -599,6 +600,7 @@ def main() -> None:
                              # the main loop and traced again in the launch's tail
                              "tie_answer": "deferred" if redo else "in the main loop",
                              "redo_samples_per_step": redo // max(args.steps, 1),
+                             "redo_late_total": redo_late,
                              "index_rule": index_rule},
     }
     print(json.dumps(out), flush=True)

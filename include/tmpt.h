@@ -133,6 +133,7 @@ typedef struct {
     int32_t tie_rule;         /* in effect: 0 octree visit order, 1 lowest index (no octree / option) */
     int64_t chain_pixels;     /* pixel seeding: pixels the last render ran as speculative chains */
     int64_t redo_samples;     /* sample seeding, tie_defer: samples the last render traced again */
+    int64_t redo_late;        /* of them, left to the second launch (the first gave up waiting) */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */

@@ -99,6 +99,9 @@ for r in range(rounds):
             assert np.array_equal(img, ref), f"variant {v!r} changed the image"
             assert rays == ref_rays, f"variant {v!r} changed the ray count ({rays} vs {ref_rays})"
         res[v].append((rays / dt / 1e6, st.extend_ms, st.shadow_ms, dt * 1e3))
+        if getattr(st, "redo_late", 0):
+            print(f"  {v or 'default'} round {r}: {st.redo_late} re-traces left to k_redo, "
+                  f"extend {st.extend_ms:.1f} ms", flush=True)
 for v, xs in res.items():
     a = np.array(xs)
     print(f"{v or 'default':>48}: {np.median(a[:, 0]):8.1f} MRays/s  extend {np.median(a[:, 1]):7.1f} ms  "

@@ -103,7 +103,7 @@ class _Stats(ctypes.Structure):
                 ("root_misses", ctypes.c_uint64), ("row_engine", ctypes.c_int32),
                 ("stream_fallbacks", ctypes.c_int32), ("octree_depth", ctypes.c_int32),
                 ("tie_rule", ctypes.c_int32), ("chain_pixels", ctypes.c_int64),
-                ("redo_samples", ctypes.c_int64)]
+                ("redo_samples", ctypes.c_int64), ("redo_late", ctypes.c_int64)]
 
 
 def _sig(name, res, args):
@@ -318,6 +318,7 @@ class RenderStats:
     tie_rule: int
     chain_pixels: int
     redo_samples: int
+    redo_late: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

@@ -847,6 +847,7 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->tie_rule = s.oct && s.opt.tie_rule == 0 ? 0 : 1;
     o->chain_pixels = s.chain_pixels;
     o->redo_samples = s.redo_samples;
+    o->redo_late = s.redo_late;
     return 0;
 }
 

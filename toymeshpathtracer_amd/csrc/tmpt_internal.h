@@ -227,6 +227,7 @@ struct Scene {
     uint2* redo = nullptr;
     uint32_t redo_cap = 0;
     int64_t redo_samples = 0;
+    int64_t redo_late = 0;   // of them, left by the launch's tail to the k_redo launch
     // speculative row seeding (tmpt_render.hip render_rowspec): jump tables
     // M^(2j) for j in [0, jt2_n), and its row/unit buffers
     uint32_t* jt2 = nullptr;

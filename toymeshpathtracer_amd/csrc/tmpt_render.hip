@@ -1375,8 +1375,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             // over the octree by the whole wave (octree_walk_wave), one after
             // another -- here, where every lane is active.  A HELP lane
             // waiting on shadow answers holds no fresh query.
+            // (the row engines, SAMP >= 2, answer in the closest-hit branch
+            // with the serial walk: the wave walk's registers spill there --
+            // row seeding 927 -> 888 MRays/s)
             bool settled = false;
-            if (!DEFER) {
+            if (!DEFER && SAMP < 2) {
                 const bool fin = has_pix && !in_query && !cam && !qany && !(HELP && waiting);
                 uint64_t T = wballot(fin && octree_tie(sv, ts));
                 if (TMPT_RARE(T != 0)) {
@@ -1433,6 +1436,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             }
                         }
                         ts.best >>= 1;  // -1 stays -1
+                    } else if (SAMP >= 2) {
+                        const bool tie = octree_tie(sv, ts);
+                        if (TMPT_RARE(wany(tie))) {
+                            if (tie) settle_closest<BLOCK, SL, true, SOA, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
+                        }
+                        if (!tie) ts.best >>= 1;
                     } else if (!settled) {
                         ts.best >>= 1;  // the index (a tie was answered above)
                     }
@@ -1731,10 +1740,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         // Redo phase: the wave's main loop is over; it traces the samples the
         // main loops dropped on ties (one per lane, by ticket), while the other
         // waves finish theirs, so the re-traces fill the frame's tail.  A lane
-        // waits on an entry only while some wave is still in its main loop (the
-        // list is final once every wave is past it); a wave that sees nothing
-        // change for kRedoPatience leaves its tickets to k_redo.
-        constexpr uint64_t kRedoPatience = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
+        // waits on an entry only while some wave of the grid is still in its
+        // main loop (the list is final once every wave is past it); a wave that
+        // sees nothing change for kRedoPatience leaves its tickets to k_redo --
+        // also the way out if the dispatcher held blocks back behind resident
+        // ones.  (Counting started waves instead of the grid cost 2 % in
+        // register allocation, measured.)
+        constexpr uint64_t kRedoPatience = 500000;  // s_memrealtime ticks (100 MHz): 5 ms
         const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
         // pc.redo_lanes lanes of the wave take tickets: a re-trace is one
         // lane's whole path, so fewer per wave spread them over more waves
@@ -2801,6 +2813,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                 TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
                 continue;
             }
+            s.redo_late = (int64_t)(std::min<unsigned long long>(n, s.redo_cap) - std::min(traced, n));
             if (traced < std::min<unsigned long long>(n, s.redo_cap)) {  // entries the launch left
                 TMPT_HIP(hipEventRecord(s.path_ev[0], s.stream));
                 k_redo<kBlk, kPathSL><<<grid, kBlk, 0, s.stream>>>(view(s), as, s.redo, s.redo_cap, pc.sbuf, pc.sb_ss,
@@ -3591,6 +3604,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.stream_fallbacks = 0;
     s.chain_pixels = 0;
     s.redo_samples = 0;
+    s.redo_late = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
