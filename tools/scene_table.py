@@ -52,7 +52,9 @@ def main():
         path = gen_standin_sponza.ensure() if obj == "sponza" else os.path.join(ROOT, "data", obj)
         tris, bmin, bmax = tm.load_scene(path)
         cam = tm.Camera.for_scene(bmin, bmax, W, H, is_sponza=sponza)
-        with tm.Scene(tris) as sc:
+        # the reference's octree (main.cpp:312): its tie order and root box,
+        # as bench.py renders (TABLE_OCTREE=0: ties by index, round-3 table)
+        with tm.Scene(tris, bounds=None if os.environ.get("TABLE_OCTREE") == "0" else (bmin, bmax)) as sc:
             cw, ch = min(W, 1920), min(H, 1080)  # visit counts on at most the 1080p frame
             ccam = tm.Camera.for_scene(bmin, bmax, cw, ch, is_sponza=sponza)
             _, q = sc.trace_image(ccam, cw, ch, 4, seed_mode=tm.SEED_SAMPLE, band_rows=1, count_visits=True)
