@@ -65,14 +65,6 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
-// a branch taken by few waves (octree tie re-answers, root-box misses): laid out
-// away from the hot loop body
-#ifdef TMPT_EXP_COLD
-#define TMPT_RARE(x) __builtin_expect(!!(x), 0)
-#else
-#define TMPT_RARE(x) (x)
-#endif
-
 // s_memtime (shader clock), for the PROF build of k_path only
 __device__ __forceinline__ uint64_t stamp()
 {
@@ -1382,7 +1374,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             if (!DEFER && SAMP < 2) {
                 const bool fin = has_pix && !in_query && !cam && !qany && !(HELP && waiting);
                 uint64_t T = wballot(fin && octree_tie(sv, ts));
-                if (TMPT_RARE(T != 0)) {
+                if (T != 0) {
                     const OctView* ov = sv.oct;
                     do {
                         const int l = (int)__builtin_ctzll(T);
@@ -1425,7 +1417,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         // once with colour x = -1 (no path colour is negative),
                         // which the colour-buffer stores below skip.
                         drop = octree_tie(sv, ts);
-                        if (TMPT_RARE(wany(drop))) {
+                        if (wany(drop)) {
                             if (drop) {
                                 const unsigned long long slot = atomicAdd(&counters[kRedoCounter], 1ull);
                                 if (slot < (unsigned long long)pc.redo_cap) pc.redo[slot] = make_uint2(pix, smp);
@@ -1438,7 +1430,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         ts.best >>= 1;  // -1 stays -1
                     } else if (SAMP >= 2) {
                         const bool tie = octree_tie(sv, ts);
-                        if (TMPT_RARE(wany(tie))) {
+                        if (wany(tie)) {
                             if (tie) settle_closest<BLOCK, SL, true, SOA, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
                         }
                         if (!tie) ts.best >>= 1;
@@ -1646,7 +1638,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
 #ifndef TMPT_EXP_NOROOT  // cost experiment: no root box test
-                if (!DEFER && TMPT_RARE(a.root_check) && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
+                if (!DEFER && a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
                     in_query = false;  // a camera ray outside the reference's root box: a counted miss
                     atomicAdd(&sv.oct->ties[1], 1ull);
                 }

@@ -422,13 +422,7 @@ __device__ __forceinline__ f3 ref_inverse(f3 d) { return mk(1.0f / d.x, 1.0f / d
 // ray from outside the root box can fail it while hitting a triangle (one
 // that grazes the root's faces at the floor's corners, main.cpp:153-162 puts
 // them on the root's boundary).
-#ifdef TMPT_EXP_CALL
-#define TMPT_WALK_INLINE __noinline__
-#else
-#define TMPT_WALK_INLINE __forceinline__
-#endif
-
-__device__ TMPT_WALK_INLINE bool root_slab(const OctNode* __restrict__ nodes, f3 o, f3 d, float tmin, float tmax)
+__device__ __forceinline__ bool root_slab(const OctNode* __restrict__ nodes, f3 o, f3 d, float tmin, float tmax)
 {
     return ref_slab(o, ref_inverse(d), nodes[0].lo, nodes[0].hi, tmin, tmax);
 }
@@ -447,14 +441,13 @@ __device__ __forceinline__ bool octree_root_hit(const SceneView& sv, f3 o, f3 d,
 // maths.cpp:341-342 forms them.  `target`: the closest t over all triangles
 // (the BVH's answer): no triangle has a smaller one, so the first met at
 // exactly `target` is the reference's answer and the walk stops there.
-// The walk itself takes plain pointers and returns by value, so it can be
-// built out of line (TMPT_EXP_CALL) without a stack frame for its results.
+// The walk itself takes plain pointers and returns by value.
 struct OctHit {
     int best;
     float t, u, v;
 };
 
-__device__ TMPT_WALK_INLINE OctHit octree_walk(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
+__device__ __forceinline__ OctHit octree_walk(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
                                                int n_oct, const TriOrig* __restrict__ tris, f3 o, f3 d,
                                                float tmin, float tmax, float target)
 {
