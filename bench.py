@@ -392,13 +392,19 @@ def main() -> None:
     ext_ms = sh_ms = 0.0
     ext_rays = sh_rays = 0
     ext_launches = 0
-    ties = roots = redo = redo_late = 0
+    ties = roots = redo = redo_late = cracks = 0
+    redo_launches = redo_rays = 0
+    redo_ms = 0.0
     for _ in range(args.steps):
         r, st = step()
         ties += st.tie_queries
         roots += st.root_misses
+        cracks += st.crack_queries
         redo += st.redo_samples
         redo_late += st.redo_late
+        redo_launches += st.redo_launches
+        redo_ms += st.redo_ms
+        redo_rays += st.redo_rays
         rays += r
         ext_ms += st.extend_ms
         sh_ms += st.shadow_ms
@@ -529,9 +535,13 @@ def main() -> None:
                   "pixel": "k_path<SAMP=0> (persistent, pixel chains; pilot + cost-ordered pass)",
                   "row": "streaming row engine: k_path<SAMP=4> speculative launch + k_path<SAMP=2> chain re-trace; "
                          "reference-chain rays only (the speculative traces are ~11x as many)"}[args.seed_mode]
-        roof = roofline((ext_rays + sh_rays) / ext_launches, ext_ms / ext_launches, b_ray, kernel,
+        # per k_path launch: its own queries and time; a k_redo launch (the
+        # deferred-tie samples the main launch's tail left) is reported apart
+        roof = roofline((ext_rays + sh_rays - redo_rays) / ext_launches, ext_ms / ext_launches, b_ray, kernel,
                         counters_apply=args.seed_mode == "sample")
-        roof.update({"n_node_per_query": round(n_node, 2), "n_tri_per_query": round(n_tri, 2)})
+        roof.update({"n_node_per_query": round(n_node, 2), "n_tri_per_query": round(n_tri, 2),
+                     "k_path_launches": ext_launches, "redo_launches": redo_launches,
+                     "redo_ms": round(redo_ms, 3), "redo_queries": redo_rays})
 
     # ---- CPU baseline: the reference algorithm on this host, bounded row sample
     cpu = None
@@ -596,6 +606,9 @@ def main() -> None:
                              "build_ms": round(st0.octree_build_ms, 1), "tie_rule": "visit" if st0.tie_rule == 0 else "index",
                              "tie_queries_per_step": ties // max(args.steps, 1),
                              "root_misses_per_step": roots // max(args.steps, 1),
+                             # hits that may lie in a crack between the octree's subtree
+                             # boxes, answered over it too
+                             "crack_queries_per_step": cracks // max(args.steps, 1),
                              # sample seeding at >= 192 samples per lane: tied samples dropped by
                              # the main loop and traced again in the launch's tail
                              "tie_answer": "deferred" if redo else "in the main loop",

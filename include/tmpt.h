@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 7  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+#define TMPT_ABI_VERSION 8  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
                               4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
                               progressive continuation keyed on the camera,
                               TMPT_SEED_SAMPLE; 6: scene options (tmpt_scene_create_ex,
@@ -33,7 +33,10 @@ extern "C" {
                               for closest hits tied on t and for rays its root box drops),
                               option tie_rule, tmpt_octree_digest, tmpt_stats octree / tie /
                               row-engine fields, tmpt_render_multi takes the octree box,
-                              options tie_defer / redo_cap, tmpt_stats.redo_samples */
+                              options tie_defer / redo_cap, tmpt_stats.redo_samples;
+                              8: the octree answers crack queries and flat triangles too
+                              (tmpt_stats.crack_queries, octree_flat), tmpt_stats.redo_launches /
+                              redo_ms (k_redo apart from the k_path launches) */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -133,7 +136,15 @@ typedef struct {
     int32_t tie_rule;         /* in effect: 0 octree visit order, 1 lowest index (no octree / option) */
     int64_t chain_pixels;     /* pixel seeding: pixels the last render ran as speculative chains */
     int64_t redo_samples;     /* sample seeding, tie_defer: samples the last render traced again */
-    int64_t redo_late;        /* of them, left to the second launch (the first gave up waiting) */
+    int64_t redo_late;        /* of them, left to the second launch (the main launch's tail did not take them) */
+    /* (ABI 8) closest-hit queries answered over the octree because they may run in one of its
+     * cracks (a hit near an octree plane on a ray nearly parallel to it) or hit a triangle
+     * lying flat on a plane (octree_flat of them in the scene); see tmpt_scene_build_octree */
+    uint64_t crack_queries;
+    int32_t octree_flat;
+    int32_t redo_launches;    /* sample seeding, tie_defer: k_redo launches of the last render (0 or 1) */
+    double redo_ms;           /* their time; extend_ms holds the main k_path launches only */
+    uint64_t redo_rays;       /* their queries (part of the render's ray count) */
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */
@@ -235,12 +246,19 @@ int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* valu
 /* Scene::BuildOctree (scene.h:26, scene.cpp:75-83; called by main.cpp:312
  * with the OBJ bounds +- 0.7 x their size): builds the reference's octree
  * (scene.cpp:99-160, host) over the scene's triangles and keeps it on the
- * device.  The BVH answers every query; the octree answers the two kinds of
- * query where the reference's answer is not the BVH's closest hit: a
+ * device.  The BVH answers every query; the octree answers the kinds of
+ * query where the reference's answer can differ from the BVH's closest hit: a
  * closest hit whose t two or more triangles share (the reference keeps the
- * first in its depth-first visit order, scene.cpp:29-48) and a ray its root
- * box test rejects (scene.cpp:25).  Without it (or with option tie_rule =
- * index) ties go to the lowest triangle index and no ray is rejected. */
+ * first in its depth-first visit order, scene.cpp:29-48), a ray its root
+ * box test rejects (scene.cpp:25), and a hit the reference's octree can miss
+ * through a crack between neighbouring subtrees (their boxes' faces differ by
+ * the rounding of min + half + half): a hit point near an octree plane on a
+ * ray nearly parallel to that plane, or a triangle lying flat on one (stats
+ * crack_queries, octree_flat).  Without it (or with option tie_rule = index)
+ * ties go to the lowest triangle index and no ray is rejected.
+ * Must not run while a render or HitScene call on the scene is in flight on
+ * another host thread: it synchronises the scene's stream and frees the old
+ * octree (a caller's wait_stream is not waited on). */
 int tmpt_scene_build_octree(tmpt_scene* scene, const float bmin[3], const float bmax[3]);
 /* The root box main.cpp:312 gives BuildOctree: sceneMin - extra, sceneMax + extra
  * with extra = (sceneMax - sceneMin) * 0.7 (main.cpp:294-295); bmin / bmax
@@ -251,6 +269,14 @@ int tmpt_octree_bounds(const float bmin[3], const float bmax[3], float box[6]);
  * the preorder walk (box bits, leaf lists)}.  Tests compare it with the
  * oracle's octree. */
 int tmpt_octree_digest(const float* tris, int32_t n, const float bmin[3], const float bmax[3], uint64_t out[5]);
+/* Check hook (host only, no device): which of n_rays answered queries the
+ * octree re-answers besides ties -- rays n_rays x {o.xyz, d.xyz}, t and ids the
+ * closest (or first) hit of each (ids < 0: a miss, never flagged):
+ * flags[i] = 1 the hit triangle lies flat on an octree plane, | 2 the hit may
+ * lie in a crack (the device's own octree_crack test).  grid (may be NULL) =
+ * {r0.xyz, 1/cell.xyz, cell.xyz, band.xyz, reach} of that octree. */
+int tmpt_octree_flags(const float* tris, int32_t n, const float bmin[3], const float bmax[3], const float* rays,
+                      const float* t, const int32_t* ids, int64_t n_rays, uint8_t* flags, float grid[13]);
 /* Scene::~Scene (scene.h:20) */
 int tmpt_scene_destroy(tmpt_scene* scene);
 

@@ -74,6 +74,10 @@ _hit_batch = _sig("orc_hit_batch", None, [ctypes.c_void_p, _f32p, ctypes.c_int64
                                           ctypes.c_float, _f32p, _i32p, ctypes.c_int32])
 _stats = _sig("orc_scene_stats", None, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)])
 _oct_digest = _sig("orc_octree_digest", ctypes.c_uint64, [ctypes.c_void_p])
+_oct_nodes = _sig("orc_octree_nodes", ctypes.c_int64, [ctypes.c_void_p, _f32p, _i32p, ctypes.c_int64])
+_oct_leaf = _sig("orc_octree_leaf", ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int64, _i32p, ctypes.c_int32])
+_ray_box = _sig("orc_ray_box_batch", None, [_f32p, ctypes.c_int64, _f32p, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_void_p])
 _render = _sig("orc_render", ctypes.c_uint64, [ctypes.c_void_p, ctypes.POINTER(_Camera), ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -197,6 +201,16 @@ def load_scene(path: str):
     return tris, bmin, bmax
 
 
+def ray_box(rays, box, t_min, t_max) -> np.ndarray:
+    """RayHitAabb (maths.h:116-134) of each ray {o, d} against box {min, max},
+    over 1/d as HitScene forms it (scene.cpp:92-93): bool per ray."""
+    rays = np.ascontiguousarray(np.asarray(rays, np.float32).reshape(-1, 6))
+    b = np.ascontiguousarray(np.asarray(box, np.float32).reshape(6))
+    out = np.zeros(rays.shape[0], np.uint8)
+    _ray_box(_fp(rays), rays.shape[0], _fp(b), t_min, t_max, out.ctypes.data)
+    return out.astype(bool)
+
+
 class Scene:
     """Oracle scene: accel = ACCEL_OCTREE (the reference's, scene.cpp:75-83, 99-160),
     ACCEL_BVH (exact linear-scan semantics, own BVH) or ACCEL_LINEAR."""
@@ -237,6 +251,24 @@ class Scene:
         """FNV-1a of the octree's preorder walk (0 for other accelerators' scenes
         it is the empty hash)."""
         return int(_oct_digest(self._h))
+
+    def octree_nodes(self):
+        """(boxes n x 6 {min, max}, info n x 3 {first child or -1, leaf
+        triangle count, depth}) of the octree in storage order."""
+        n = int(_oct_nodes(self._h, None, None, 0))
+        boxes = np.zeros((n, 6), np.float32)
+        info = np.zeros((n, 3), np.int32)
+        if n:
+            _oct_nodes(self._h, _fp(boxes), info.ctypes.data_as(_i32p), n)
+        return boxes, info
+
+    def octree_leaf(self, node: int) -> np.ndarray:
+        """Triangle ids of leaf `node`, in the reference's order."""
+        n = int(_oct_leaf(self._h, node, None, 0))
+        ids = np.zeros(n, np.int32)
+        if n:
+            _oct_leaf(self._h, node, ids.ctypes.data_as(_i32p), n)
+        return ids
 
     def render(self, cam_arr, w, h, spp, seed_mode=SEED_ROW, y0=0, y1=None, row_step=1,
                threads=None, rgba=None, x0=0, x_step=1):

@@ -708,6 +708,47 @@ uint64_t orc_octree_digest(const orc_scene* s)
     return h;
 }
 
+static void oct_depths(const orc_scene* s, int64_t node, int32_t depth, int32_t* info, int64_t cap)
+{
+    if (node < cap) info[3 * node + 2] = depth;
+    const oct_node* nd = &s->oct[node];
+    if (nd->first_child >= 0)
+        for (int i = 0; i < 8; ++i) oct_depths(s, nd->first_child + i, depth + 1, info, cap);
+}
+
+int64_t orc_octree_nodes(const orc_scene* s, float* boxes, int32_t* info, int64_t cap)
+{
+    if (s->accel != ORC_ACCEL_OCTREE) return 0;
+    const int64_t m = s->n_oct < cap ? s->n_oct : cap;
+    for (int64_t i = 0; i < m; ++i) {
+        const oct_node* nd = &s->oct[i];
+        vstore(boxes + 6 * i, nd->bmin);
+        vstore(boxes + 6 * i + 3, nd->bmax);
+        info[3 * i] = nd->first_child;
+        info[3 * i + 1] = nd->first_child < 0 ? nd->tri_cnt : 0;
+    }
+    if (s->n_oct > 0 && m > 0) oct_depths(s, 0, 0, info, m);
+    return s->n_oct;
+}
+
+int32_t orc_octree_leaf(const orc_scene* s, int64_t node, int32_t* ids, int32_t cap)
+{
+    if (s->accel != ORC_ACCEL_OCTREE || node < 0 || node >= s->n_oct || s->oct[node].first_child >= 0) return 0;
+    const oct_node* nd = &s->oct[node];
+    for (int32_t k = 0; k < nd->tri_cnt && k < cap; ++k) ids[k] = s->oct_tris[nd->tri_off + k];
+    return nd->tri_cnt;
+}
+
+void orc_ray_box_batch(const float* rays, int64_t n, const float box[6], float tmin, float tmax, uint8_t* out)
+{
+    const v3 lo = vload(box), hi = vload(box + 3);
+    for (int64_t i = 0; i < n; ++i) {
+        const v3 o = vload(rays + 6 * i), d = vload(rays + 6 * i + 3);
+        const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); /* scene.cpp:92-93 */
+        out[i] = (uint8_t)ray_hit_aabb(o, inv, lo, hi, tmin, tmax);
+    }
+}
+
 /* Scene::HitScene, scene.cpp:86-97 (returns the triangle index, not 1) */
 static int32_t hit_scene(const orc_scene* s, v3 ro, v3 rd, float tMin, float tMax, hit_t* out)
 {

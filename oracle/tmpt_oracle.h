@@ -88,6 +88,17 @@ void       orc_hit_batch(const orc_scene* s, const float* rays, int64_t n, float
 void       orc_scene_stats(const orc_scene* s, int64_t out[4]);
 /* FNV-1a of the octree's preorder walk (box bits, leaf lists): see the C file */
 uint64_t   orc_octree_digest(const orc_scene* s);
+/* The octree's nodes in storage order (the root first, each node's 8 children
+ * contiguous): boxes n x {min.xyz, max.xyz}, info n x {first child or -1,
+ * leaf triangle count, depth}.  Writes min(n, cap) nodes; returns n.  Test
+ * generators aim rays at these boxes' faces, edges and corners. */
+int64_t    orc_octree_nodes(const orc_scene* s, float* boxes, int32_t* info, int64_t cap);
+/* A leaf's triangle list in the reference's order (ids[0..min(count, cap))); returns its count */
+int32_t    orc_octree_leaf(const orc_scene* s, int64_t node, int32_t* ids, int32_t cap);
+/* The reference's slab test (maths.h:116-134 over 1/dir, scene.cpp:92-93) of
+ * each ray against one box: out[i] = 1 if RayHitAabb passes. */
+void       orc_ray_box_batch(const float* rays, int64_t n, const float box[6], float tmin, float tmax,
+                             uint8_t* out);
 
 /* ---- Tracer (main.cpp:44-119, 172-246) ----
  * Renders rows y = y0, y0+row_step, ... < y1 into rgba (full-frame layout,

@@ -47,7 +47,7 @@ def test_no_oracle_or_torch_in_the_product_library():
 
 
 def test_abi_version_and_error_channel():
-    assert tm.abi_version() == 7
+    assert tm.abi_version() == 8
     with pytest.raises(tm.TmptError) as e:
         tm.load_scene("/definitely/missing.obj")
     assert "missing.obj" in str(e.value)

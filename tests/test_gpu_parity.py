@@ -458,20 +458,50 @@ def test_sponza_standin_rows_match_oracle(gpu, sponza_path):
 
 
 def test_full_size_teapot_engine_independence(gpu):
-    """configs[2] at full size: wavefront == megakernel byte for byte, same
-    ray count (a size-independent property); a row sample against the oracle."""
-    tris, bmin, bmax, sc = _scene("teapot.obj")
+    """configs[2] at full size (teapot 1280x720x16) with the reference's
+    octree built, as the product's CLI and bench build it (main.cpp:312):
+    wavefront == megakernel == persistent byte for byte with the same ray
+    count (a size-independent property), every 48th row equal to the
+    reference algorithm (oracle octree, visit-order ties) in pixel seeding,
+    and the sample-seeded frame's rows too."""
+    tris, bmin, bmax, sc = _scene("teapot.obj", octree=True)
     w, h, spp = 1280, 720, 16
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
     a, ra = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_WAVEFRONT)
     b, rb = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_MEGAKERNEL)
     c, rc = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, engine=tm.ENGINE_PERSISTENT)
+    assert sc.stats().tie_rule == 0
     assert ra == rb == rc and np.array_equal(a, b) and np.array_equal(a, c)
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
-    ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL, row_step=48)
+    smp, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
+    osc = _ref_oracle(tris, bmin, bmax)
     rows = np.arange(0, h, 48)
-    assert np.array_equal(a[rows], ref[rows])
+    ref, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL, row_step=48)
+    diff = np.nonzero((a[rows] != ref[rows]).any(-1))
+    assert diff[0].size == 0, f"pixel: {diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+    ref_s, _ = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE, row_step=48)
+    diff = np.nonzero((smp[rows] != ref_s[rows]).any(-1))
+    assert diff[0].size == 0, f"sample: {diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
     sc.close()
+
+
+def test_pixel_bench_frame_full_spp_octree_vs_oracle(gpu, sponza_path):
+    """The bench frame (stand-in sponza 1920x1080) at its full 64 spp in PIXEL
+    seeding (bench.py's seed_modes.pixel line: the pilot-ordered persistent
+    engine) with the reference's octree built: every 64th row equals the
+    reference algorithm (oracle octree, visit-order ties) byte for byte, and
+    the octree answered queries (ties met)."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 64
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1)
+        st = sc.stats()
+    assert st.tie_rule == 0 and st.tie_queries > 0
+    rows = np.arange(0, h, 64)
+    ref, _ = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_PIXEL,
+                                                  row_step=64)
+    diff = np.nonzero((img[rows] != ref[rows]).any(-1))
+    assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
 
 
 def test_device_output_pointer(gpu):
@@ -910,15 +940,18 @@ def test_sponza4k_config4_shard_oracle_and_fallback(gpu, sponza_path):
         dealt round-robin) equals those rows of the single-GPU frame, and the
         8 shards' rays add up to the frame's;
     (b) 3 rows of the full frame equal the oracle's row loop at 256 spp
-        (main.cpp:202-233), byte for byte;
+        (main.cpp:202-233) over the reference's octree (visit-order ties),
+        byte for byte -- the octree is built, as bench.py --config sponza4k
+        builds it;
     (c) the same frame with the per-sample colour buffer capped (option
         sbuf_max: the path a frame too large for HBM takes -- here the buffer
         is 34 GB) renders whole pixels as units: the same bytes, same rays."""
     tris, bmin, bmax = tm.load_scene(sponza_path)
     w, h, spp = 3840, 2160, 256
     cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
-    with tm.Scene(tris) as sc:
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:  # the reference's octree, as bench.py builds it
         full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
+        assert sc.stats().tie_rule == 0 and sc.stats().tie_queries > 0
         total = 0
         for k in range(8):
             tile, r = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1, shard=k, num_shards=8)
@@ -928,7 +961,7 @@ def test_sponza4k_config4_shard_oracle_and_fallback(gpu, sponza_path):
         sc.set_option("sbuf_max", 1 << 20)
         capped, rays_c = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
         assert rays_c == rays and np.array_equal(capped, full)
-    osc = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    osc = _ref_oracle(tris, bmin, bmax)
     rows = np.array([5, 1080, 2150])
     ref = np.zeros((h, w, 4), np.uint8)
     for y in rows:
@@ -1062,4 +1095,89 @@ def test_pixel_chains_match_oracle(gpu, per1024):
     assert rays == ref_rays and np.array_equal(img, ref)
     tile, trays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL, band_rows=1, shard=1, num_shards=3)
     assert np.array_equal(tile, ref[1::3])
+    sc.close()
+
+
+# ---------------------------------------------------------------- the octree's cracks
+@pytest.mark.parametrize("name", ["cube", "suzanne", "teapot", "grid", "crack_wall"])
+def test_hitscene_adversarial_octree(gpu, name):
+    """HitScene on rays aimed at the reference octree's faces, edges and
+    corners, at triangles crossing them, along them (axis-parallel and
+    in-plane rays: the crack class) and at vertices (tests/octree_kat.py);
+    'grid' puts its geometry on the octree's planes, 'crack_wall' adds a wall
+    lying inside one of teapot's cracks (in no leaf: the reference sees
+    through it).  The GPU's answers equal the reference algorithm's (oracle
+    octree) on every ray -- ties, root-box misses and crack queries included --
+    and the any-hit query's hit bit equals it.  Reports the deviation counts."""
+    import octree_kat as K
+    if name == "grid":
+        tris, bmin, bmax = K.grid_scene()
+    else:
+        tris, bmin, bmax = oracle.load_scene(data(("teapot" if name == "crack_wall" else name) + ".obj"))
+    extra = None
+    if name == "crack_wall":
+        tris, ax, _ = K.crack_wall_scene(tris, bmin, bmax)
+        extra = K.crack_wall_rays(tris[-1], ax, 4000, seed=3)
+    osc = K.ref_scene(tris, bmin, bmax)
+    rays, kind = K.adversarial_rays(tris, bmin, bmax, 8000, seed=9, osc=osc)
+    if extra is not None:
+        rays = np.concatenate([rays, extra])
+    c = K.classify(tris, bmin, bmax, rays, osc=osc)
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
+        st = sc.stats()
+        aids, _ = sc.hit_scene_batch(rays, 0.001, 1.0e7, any_hit=True)
+    print(name, "rays", len(rays), "ties", len(c["tie"]), "root", len(c["root"]), "crack class", len(c["other"]),
+          "gpu tie_queries", st.tie_queries, "crack_queries", st.crack_queries, "flat", st.octree_flat)
+    _same_answers(ids, hits, c["rid"], c["rh"])
+    assert np.array_equal(aids >= 0, c["rid"] >= 0)
+    if name in ("teapot", "crack_wall"):
+        assert len(c["other"]) > 0 and st.crack_queries + st.tie_queries >= len(c["other"])
+    if name == "crack_wall":
+        assert st.octree_flat == 1
+
+
+@pytest.mark.parametrize("engine", [tm.ENGINE_PERSISTENT, tm.ENGINE_WAVEFRONT, tm.ENGINE_MEGAKERNEL])
+@pytest.mark.parametrize("seed,oseed", [(tm.SEED_PIXEL, oracle.SEED_PIXEL), (tm.SEED_SAMPLE, oracle.SEED_SAMPLE),
+                                        (tm.SEED_ROW, oracle.SEED_ROW)])
+def test_crack_wall_render(gpu, engine, seed, oseed):
+    """A frame looking at a wall that lies inside a crack of teapot's octree
+    (in no leaf, so the reference's camera and shadow rays pass through it):
+    every engine and seeding gives the reference algorithm's frame (oracle
+    octree) byte for byte -- the wall's hits are flagged (a flat triangle) and
+    answered over the octree, shadow queries included (PathCtl::oct_shadow)."""
+    import octree_kat as K
+    tris, bmin, bmax = oracle.load_scene(data("teapot.obj"))
+    tris, ax, p = K.crack_wall_scene(tris, bmin, bmax)
+    frm = p.astype(np.float64).copy()
+    frm[ax] -= 3.0
+    frm[(ax + 1) % 3] += 0.7
+    w, h, spp = 96, 64, 3
+    cam = tm.Camera.create(frm.astype(np.float32), p, [0, 1, 0] if ax != 1 else [1, 0, 0], 20.0, w / h, 0.0, 3.0)
+    ref, ref_rays = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oseed)
+    exact, _ = oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax).render(
+        cam.as_array(), w, h, spp, seed_mode=oseed)
+    assert not np.array_equal(ref, exact)  # the wall is in view: the reference sees through it
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=seed, engine=engine)
+        st = sc.stats()
+    assert st.octree_flat == 1
+    assert rays == ref_rays
+    diff = np.nonzero((img != ref).any(-1))
+    assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+
+
+def test_hitscene_negative_single_range(gpu):
+    """one range for the batch that starts behind the origin
+    (t_min = -1e7): the traversal's far-distance slack by magnitude (NEG), so
+    no box behind the origin is culled -- the same answers as the oracle's
+    linear scan."""
+    tris, bmin, bmax, sc = _scene("suzanne.obj")
+    rays = _random_rays(tris, 40_000, seed=31)
+    for lo, hi in ((-1.0e7, 1.0e7), (-3.0, 0.5)):
+        ids, hits = sc.hit_scene_batch(rays, lo, hi)
+        oids, ohits = oracle.Scene(tris, accel=oracle.ACCEL_LINEAR).hit_batch(rays, lo, hi)
+        assert (ids >= 0).sum() > 1000 and np.array_equal(ids, oids), (lo, hi)
+        h = ids >= 0
+        assert np.array_equal(hits[h].view(np.uint32), ohits[h].view(np.uint32))
     sc.close()

@@ -1,0 +1,96 @@
+"""The reference's octree against the exact closest hit, on rays aimed at its
+cracks (CPU, oracle + the library's host check hook; no GPU).
+
+The library answers closest hits from its BVH and sends to the reference's
+octree only the queries where the two can differ.  tests/octree_kat.py aims
+rays at the octree's own faces, edges and corners, at triangles crossing them,
+along them (axis-parallel and in-plane directions) and at triangle vertices,
+and sorts every difference between the reference's answer (oracle octree,
+visit order, scene.cpp:21-52) and the exact closest hit into ties, root-box
+misses and the rest.  The rest is the crack class (tmpt_internal.h OctGrid):
+this test checks that the library's own predicate (tmpt_octree_flags, the
+device's octree_crack and the flat-triangle marks) flags every such ray, so
+the GPU answers it over the octree (tests/test_gpu_parity.py checks that).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import octree_kat as K
+import toymeshpathtracer_amd as tm
+from conftest import data
+
+
+def _scene(name):
+    if name == "grid":
+        return K.grid_scene()
+    return oracle.load_scene(data(name + ".obj"))
+
+
+@pytest.mark.parametrize("name", ["cube", "suzanne", "teapot", "grid"])
+def test_excluded_class_is_flagged(name):
+    tris, bmin, bmax = _scene(name)
+    osc = K.ref_scene(tris, bmin, bmax)
+    rays, kind = K.adversarial_rays(tris, bmin, bmax, 6000, seed=5, osc=osc)
+    c = K.classify(tris, bmin, bmax, rays, osc=osc)
+    lo, hi = tm.octree_bounds(bmin, bmax)
+    flags, grid = tm.octree_flags(tris, lo, hi, rays, c["eh"][:, 6], c["eid"])
+    other = c["other"]
+    per_kind = {K.KINDS[k]: int((kind[other] == k).sum()) for k in range(len(K.KINDS))}
+    print(name, "rays", c["n"], "ties", len(c["tie"]), "root", len(c["root"]), "other", len(other), per_kind,
+          "flagged", int((flags > 0).sum()))
+    assert c["hits"] > c["n"] // 2
+    unflagged = other[flags[other] == 0]
+    assert unflagged.size == 0, f"{unflagged.size} unflagged deviations, first {rays[unflagged[:3]]}"
+    if name == "teapot":  # the class exists: axis-parallel and in-plane rays along a crack
+        assert len(other) > 0 and per_kind["axis_edge"] + per_kind["axis_face"] + per_kind["in_plane"] == len(other)
+
+
+def test_near_parallel_rays_flagged():
+    """Rays leaving an octree plane with one direction component 1e-7 .. 1e-2
+    (the drift that decides whether a ray can run inside a crack): every
+    deviation from the exact closest hit that is not a tie or a root miss is
+    flagged."""
+    tris, bmin, bmax = _scene("teapot")
+    osc = K.ref_scene(tris, bmin, bmax)
+    boxes, _ = osc.octree_nodes()
+    rng = np.random.default_rng(1)
+    v = tris.reshape(-1, 3)
+    lo, hi = v.min(0), v.max(0)
+    n, total_other = 4000, 0
+    olo, ohi = tm.octree_bounds(bmin, bmax)
+    for mag in (0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-2):
+        o = K._origins(rng, lo, hi, n)
+        ax, ar = rng.integers(0, 3, n), np.arange(n)
+        b = boxes[rng.integers(0, len(boxes), n)]
+        o[ar, ax] = b[ar, ax + 3 * rng.integers(0, 2, n)]
+        d = K._unit(K._box_points(rng, boxes, n, "face") - o)
+        d[ar, ax] = mag * rng.choice([-1.0, 1.0], n) * (1 + rng.random(n))
+        rays = np.concatenate([o, K._unit(d)], 1).astype(np.float32)
+        c = K.classify(tris, bmin, bmax, rays, osc=osc)
+        flags, _ = tm.octree_flags(tris, olo, ohi, rays, c["eh"][:, 6], c["eid"])
+        assert (flags[c["other"]] > 0).all(), mag
+        total_other += len(c["other"])
+    assert total_other > 0
+
+
+def test_crack_wall_is_flat_and_lost():
+    """A wall lying inside a crack of teapot's octree (in no leaf): the
+    reference sees through it -- every ray aimed at it answers differently
+    from the exact closest hit -- and the library marks it flat, so every hit
+    on it is flagged."""
+    tris, bmin, bmax = _scene("teapot")
+    got = K.crack_wall_scene(tris, bmin, bmax)
+    assert got is not None
+    t2, ax, _ = got
+    rays = K.crack_wall_rays(t2[-1], ax, 2000, seed=3)
+    c = K.classify(t2, bmin, bmax, rays)
+    wall = len(t2) - 1
+    assert (c["eid"] == wall).sum() > 1500 and (c["rid"] == wall).sum() == 0
+    lo, hi = tm.octree_bounds(bmin, bmax)
+    flags, _ = tm.octree_flags(t2, lo, hi, rays, c["eh"][:, 6], c["eid"])
+    on_wall = c["eid"] == wall
+    assert (flags[on_wall] & 1).all() and (flags[c["other"]] > 0).all()
+    # the scene's own triangles are not flat (teapot has no triangle on a plane)
+    f_all, _ = tm.octree_flags(tris, lo, hi, rays[:1], np.ones(1, np.float32), np.zeros(1, np.int32))
+    assert f_all[0] & 1 == 0

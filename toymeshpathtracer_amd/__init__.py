@@ -30,7 +30,7 @@ import numpy as np
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
     "SEED_ROW", "SEED_PIXEL", "SEED_SAMPLE", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
-    "tile_rows", "tile_row_to_y", "render_multi", "octree_bounds", "octree_digest",
+    "tile_rows", "tile_row_to_y", "render_multi", "octree_bounds", "octree_digest", "octree_flags",
 ]
 
 SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
@@ -103,7 +103,10 @@ class _Stats(ctypes.Structure):
                 ("root_misses", ctypes.c_uint64), ("row_engine", ctypes.c_int32),
                 ("stream_fallbacks", ctypes.c_int32), ("octree_depth", ctypes.c_int32),
                 ("tie_rule", ctypes.c_int32), ("chain_pixels", ctypes.c_int64),
-                ("redo_samples", ctypes.c_int64), ("redo_late", ctypes.c_int64)]
+                ("redo_samples", ctypes.c_int64), ("redo_late", ctypes.c_int64),
+                ("crack_queries", ctypes.c_uint64), ("octree_flat", ctypes.c_int32),
+                ("redo_launches", ctypes.c_int32), ("redo_ms", ctypes.c_double),
+                ("redo_rays", ctypes.c_uint64)]
 
 
 def _sig(name, res, args):
@@ -139,6 +142,8 @@ _render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Ca
 _build_octree = _sig("tmpt_scene_build_octree", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p])
 _octree_bounds = _sig("tmpt_octree_bounds", ctypes.c_int, [_f32p, _f32p, _f32p])
 _octree_digest = _sig("tmpt_octree_digest", ctypes.c_int, [_f32p, ctypes.c_int32, _f32p, _f32p, _u64p])
+_octree_flags = _sig("tmpt_octree_flags", ctypes.c_int, [_f32p, ctypes.c_int32, _f32p, _f32p, _f32p, _f32p, _i32p,
+                                                         ctypes.c_int64, ctypes.c_void_p, _f32p])
 _render_multi = _sig("tmpt_render_multi", ctypes.c_int,
                      [_f32p, ctypes.c_int32, _f32p, ctypes.POINTER(_Camera), ctypes.POINTER(_Desc),
                       ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.c_void_p, _u64p,
@@ -158,7 +163,8 @@ EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_sc
            "tmpt_scene_get_option", "tmpt_scene_destroy", "tmpt_scene_hit", "tmpt_scene_hit_ranged",
            "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
            "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos",
-           "tmpt_scene_build_octree", "tmpt_octree_bounds", "tmpt_octree_digest")
+           "tmpt_scene_build_octree", "tmpt_octree_bounds", "tmpt_octree_digest",
+           "tmpt_octree_flags")
 
 
 def _check(rc: int, what: str) -> None:
@@ -222,6 +228,23 @@ def octree_digest(tris: np.ndarray, box_min, box_max) -> dict:
     out = (ctypes.c_uint64 * 5)()
     _check(_octree_digest(_fp(t), t.shape[0], _fp(lo), _fp(hi), out), "octree_digest")
     return dict(zip(("nodes", "leaves", "refs", "depth", "digest"), (int(v) for v in out)))
+
+
+def octree_flags(tris: np.ndarray, box_min, box_max, rays, t, ids):
+    """Which answered queries the octree re-answers besides ties (host, no GPU):
+    per ray 1 = the hit triangle lies flat on an octree plane, 2 = the hit may
+    lie in a crack (the device's test), 0 = the BVH's answer stands; and the
+    crack grid {r0, 1/cell, cell, band, reach}."""
+    tr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    lo, hi = np.asarray(box_min, np.float32), np.asarray(box_max, np.float32)
+    r = np.ascontiguousarray(np.asarray(rays, np.float32)[:, :6])
+    tt = np.ascontiguousarray(np.asarray(t, np.float32))
+    ii = np.ascontiguousarray(np.asarray(ids, np.int32))
+    out = np.zeros(r.shape[0], np.uint8)
+    grid = np.zeros(13, np.float32)
+    _check(_octree_flags(_fp(tr), tr.shape[0], _fp(lo), _fp(hi), _fp(r), _fp(tt), ii.ctypes.data_as(_i32p),
+                         r.shape[0], out.ctypes.data, _fp(grid)), "octree_flags")
+    return out, grid
 
 
 # ----------------------------------------------------------------------------- camera
@@ -319,6 +342,11 @@ class RenderStats:
     chain_pixels: int
     redo_samples: int
     redo_late: int
+    crack_queries: int
+    octree_flat: int
+    redo_launches: int
+    redo_ms: float
+    redo_rays: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

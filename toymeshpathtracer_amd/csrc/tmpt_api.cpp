@@ -14,6 +14,7 @@
 
 #include "tmpt.h"
 #include "tmpt_internal.h"
+#include "tmpt_traverse.h"
 
 namespace tmpt {
 
@@ -463,7 +464,18 @@ int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax
         (void)hipFree(d_refs);
         return (set_error("tmpt_scene_build_octree: out of device memory"), -1);
     }
-    const OctView ov{d_nodes, d_refs, (int32_t)t.nodes.size(), s.ties};
+    // the crack grid and the flat triangles (tmpt_internal.h OctGrid), marked
+    // in the BVH's triangle records so that a hit on one flags its query
+    OctGrid grid;
+    octree_grid(t, bmin, bmax, grid);
+    std::vector<uint8_t> flat;
+    const int32_t n_flat = octree_flat_triangles(s.tris_host.data(), s.n, grid, flat);
+    if (mark_flat_triangles(s, flat)) {
+        (void)hipFree(d_nodes);
+        (void)hipFree(d_refs);
+        return -1;
+    }
+    const OctView ov{d_nodes, d_refs, (int32_t)t.nodes.size(), n_flat, s.ties, grid};
     if (hipMemcpy(s.oct_view, &ov, sizeof(ov), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d_nodes);
         (void)hipFree(d_refs);
@@ -477,6 +489,8 @@ int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax
     s.n_oct_refs = (int64_t)t.refs.size();
     s.oct_leaves = t.leaves;
     s.oct_depth = t.depth;
+    s.oct_flat = n_flat;
+    s.oct_grid = grid;
     for (int c = 0; c < 3; ++c) {
         s.oct_lo[c] = bmin[c];
         s.oct_hi[c] = bmax[c];
@@ -507,6 +521,39 @@ int tmpt_octree_digest(const float* tris, int32_t n, const float bmin[3], const 
     out[2] = t.refs.size() - (uint64_t)t.leaves;  // triangle references (the count words excluded)
     out[3] = (uint64_t)t.depth;
     out[4] = octree_digest(t);
+    return 0;
+    TMPT_GUARD_END
+}
+
+int tmpt_octree_flags(const float* tris, int32_t n, const float bmin[3], const float bmax[3], const float* rays,
+                      const float* t, const int32_t* ids, int64_t n_rays, uint8_t* flags, float grid[13])
+{
+    TMPT_GUARD_BEGIN
+    if (n < 0 || (n > 0 && !tris) || !bmin || !bmax || n_rays < 0 || (n_rays > 0 && (!rays || !t || !ids || !flags)))
+        return bad("tmpt_octree_flags: bad arguments");
+    OctreeHost oh;
+    build_octree(tris, n, bmin, bmax, oh);
+    OctGrid g;
+    octree_grid(oh, bmin, bmax, g);
+    std::vector<uint8_t> flat;
+    octree_flat_triangles(tris, n, g, flat);
+    for (int64_t i = 0; i < n_rays; ++i) {
+        const float* r = rays + 6 * i;
+        const int32_t id = ids[i];
+        uint8_t f = 0;
+        if (id >= 0 && id < n)
+            f = (uint8_t)(flat[(size_t)id] | (octree_crack(g, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), t[i]) ? 2 : 0));
+        flags[i] = f;
+    }
+    if (grid) {
+        for (int k = 0; k < 3; ++k) {
+            grid[k] = g.r0[k];
+            grid[3 + k] = g.inv_cell[k];
+            grid[6 + k] = g.cell[k];
+            grid[9 + k] = g.band[k];
+        }
+        grid[12] = g.reach;
+    }
     return 0;
     TMPT_GUARD_END
 }
@@ -561,6 +608,7 @@ int scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, fl
     if (!rc) {
         s.tie_queries = s.counters_host[kTieCounter];
         s.root_misses = s.counters_host[kTieCounter + 1];
+        s.crack_queries = s.counters_host[kCrackCounter];
     }
     cleanup();
     return rc;
@@ -848,6 +896,11 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->chain_pixels = s.chain_pixels;
     o->redo_samples = s.redo_samples;
     o->redo_late = s.redo_late;
+    o->crack_queries = s.crack_queries;
+    o->octree_flat = s.oct ? s.oct_flat : 0;
+    o->redo_launches = s.redo_launches;
+    o->redo_ms = s.redo_ms;
+    o->redo_rays = s.redo_rays;
     return 0;
 }
 

@@ -695,7 +695,43 @@ __global__ void __launch_bounds__(kBlock) k_soa_planes(const Bvh4Node* __restric
     }
 }
 
+// The octree's flat triangles (tmpt_internal.h OctGrid): bit 0 of the doubled
+// index in the leaf-ordered records (and the SoA plane) set where flat[index],
+// cleared elsewhere, so an accepted flat triangle flags its query.
+__global__ void __launch_bounds__(kBlock) k_mark_flat(TriPre* __restrict__ pre, float2* __restrict__ tc, int32_t n,
+                                                      const uint8_t* __restrict__ flat)
+{
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= n) return;
+    const int w = __float_as_int(pre[k].c.y);
+    const int v = (w & ~1) | (flat ? (int)flat[w >> 1] : 0);
+    pre[k].c.y = __int_as_float(v);
+    if (tc) tc[k].y = __int_as_float(v);
+}
+
 }  // namespace
+
+int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat)
+{
+    if (s.n <= 0) return 0;
+    uint8_t* d = nullptr;
+    const bool any = std::find(flat.begin(), flat.end(), (uint8_t)1) != flat.end();
+    if (any) {
+        TMPT_HIP(hipMalloc(&d, (size_t)s.n));
+        if (hipMemcpy(d, flat.data(), (size_t)s.n, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            set_error("mark_flat_triangles: upload failed");
+            return -1;
+        }
+    }
+    k_mark_flat<<<blocks_for(s.n, kBlock), kBlock, 0, s.stream>>>(s.tri_pre, const_cast<float2*>(s.soa.tc), s.n, d);
+    const hipError_t e = hipGetLastError();
+    const hipError_t e2 = hipStreamSynchronize(s.stream);
+    if (d) (void)hipFree(d);
+    TMPT_HIP(e);
+    TMPT_HIP(e2);
+    return 0;
+}
 
 int build_soa(Scene& s)
 {

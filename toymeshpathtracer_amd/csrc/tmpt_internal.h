@@ -69,14 +69,40 @@ struct alignas(16) OctNode {
 };
 static_assert(sizeof(OctNode) == 32, "octree node: two dwordx4 loads");
 
+// The octree's cracks ("cracks"): a child box is its
+// parent's min plus half the parent's size, its max that plus half again, so
+// the boxes of two neighbouring subtrees need not share a face bit for bit --
+// one subtree can end an ulp or two before the next begins.  A ray that runs
+// inside such a gap, nearly parallel to it, passes no leaf there, and the
+// reference misses a triangle the exact closest hit finds; a triangle lying
+// flat inside a gap is in no leaf at all.  The planes of the octree are the
+// grid r0 + j * cell (cell = root size / 2^depth) to within `band`, so the
+// queries that can land in a gap are known from the hit alone:
+//   crack  hit point within band[k] of a plane of axis k, and the ray moved
+//          less than 2 band[k] along k over min(t, reach) -- it ran along
+//          the gap -- for some axis k;
+//   flat   the hit triangle lies within 2 band[k] of one plane (its TriPre
+//          index is odd: marked when the octree is built).
+// Both are answered over the octree, as ties are.
+struct OctGrid {
+    float r0[3];        // root box min
+    float inv_cell[3];  // 2^depth / root size
+    float cell[3];      // root size / 2^depth
+    float band[3];      // 4 x the largest plane offset of any node box + 8 ulp of the root's coordinates
+    float reach;        // half the smallest cell: t beyond which a ray's drift along k is judged
+};
+
 // What the kernels see of it (one device-side struct, so a kernel keeps one
 // pointer live): nodes, leaf lists, node count, the counters of the queries
-// it answered ([0] ties, [1] root-box misses; Scene::ties).
+// it answered ([0] ties, [1] root-box misses, [6] crack / flat-triangle
+// queries; Scene::ties), the crack grid.
 struct OctView {
     const OctNode* nodes;
     const int32_t* refs;
     int32_t n;
+    int32_t flat;  // triangles marked flat (0: the any-hit answers need no check)
     unsigned long long* ties;
+    OctGrid grid;
 };
 
 struct OctreeHost {
@@ -91,6 +117,10 @@ void build_octree(const float* tris9, int32_t n, const float bmin[3], const floa
 // FNV-1a over the preorder walk (node boxes' bits, leaf triangle lists): the
 // structure check the CPU tests compare with the oracle's octree
 uint64_t octree_digest(const OctreeHost& t);
+// The crack grid of an octree (tmpt_octree.cpp) and the triangles that lie
+// flat on one of its planes (flat[i] = 1).
+void octree_grid(const OctreeHost& t, const float bmin[3], const float bmax[3], OctGrid& g);
+int32_t octree_flat_triangles(const float* tris9, int32_t n, const OctGrid& g, std::vector<uint8_t>& flat);
 
 // Build option layout=soa (the north star's "SoA" A/B):
 // the BVH4Q nodes and the leaf-ordered triangle records as planes, each plane
@@ -122,7 +152,10 @@ constexpr int kStackTotal = 128;
 
 constexpr int kRowSpecMaxGroups = 8;  // speculative row engine: row groups (streams)
 constexpr int kRenderCounters = 32;   // ray / visit / round counters of one render
-constexpr int kTieCounter = 24;       // [24] tied queries re-answered over the octree, [25] root-box misses
+constexpr int kTieCounter = 24;       // [24] tied queries re-answered over the octree, [25] root-box misses,
+                                      // [30] crack / flat-triangle queries re-answered over it (ties[6])
+constexpr int kCrackCounter = 30;
+constexpr int kRedoRaysCounter = 31;  // rays of the k_redo launch (part of [0])
 constexpr int kRedoCounter = 26;      // samples the deferred-tie sample kernel left to the redo pass
 
 // Per-scene options: the library's control plane in place of environment
@@ -190,11 +223,13 @@ struct Scene {
     int32_t* oct_refs = nullptr;
     OctView* oct_view = nullptr;  // device copy of {oct, oct_refs, n_oct, ties}
     int32_t n_oct = 0, oct_leaves = 0, oct_depth = 0;
+    int32_t oct_flat = 0;  // triangles flat on one of the octree's planes (OctView::flat)
+    OctGrid oct_grid{};    // its crack grid (OctView::grid)
     int64_t n_oct_refs = 0;
     double oct_build_ms = 0.0;
     float oct_lo[3] = {0, 0, 0}, oct_hi[3] = {0, 0, 0};
     unsigned long long* ties = nullptr;  // [0] re-answered ties, [1] root-box misses
-    uint64_t tie_queries = 0, root_misses = 0;
+    uint64_t tie_queries = 0, root_misses = 0, crack_queries = 0;
     // row seeding: the engine of the last render (0 none, 1 one lane per row,
     // 2 iterated speculative, 3 streaming) and whether the streaming engine's
     // launch aborted and was re-rendered by the iterated one
@@ -228,6 +263,9 @@ struct Scene {
     uint32_t redo_cap = 0;
     int64_t redo_samples = 0;
     int64_t redo_late = 0;   // of them, left by the launch's tail to the k_redo launch
+    int32_t redo_launches = 0;  // k_redo launches of the last render
+    double redo_ms = 0.0;       // and their time (not in extend_ms)
+    uint64_t redo_rays = 0;     // and their rays (in the render's count)
     // speculative row seeding (tmpt_render.hip render_rowspec): jump tables
     // M^(2j) for j in [0, jt2_n), and its row/unit buffers
     uint32_t* jt2 = nullptr;
@@ -273,6 +311,9 @@ const char* last_error();
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
 int build_soa(Scene& s);  // layout=soa planes from the built AoS records
+// the octree's flat triangles marked in the leaf-ordered records (bit 0 of the
+// doubled index), the others cleared; flat has s.n entries (empty: clear all)
+int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat);
 // tmpt_render.hip: the scene's counters, pinned copy and render events (once)
 int ensure_counters(Scene& s);
 // tmpt_render.hip: sample_seed's byte tables for samples [0, spp) (1024 words each)

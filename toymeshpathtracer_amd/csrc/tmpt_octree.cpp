@@ -217,6 +217,60 @@ void build_octree(const float* tris9, int32_t n, const float bmin[3], const floa
     }
 }
 
+// The crack grid (tmpt_internal.h OctGrid): every node box face lies on a plane
+// r0 + j * cell of the finest level to within the largest offset found here
+// (the rounding of min + half + half down the tree); the band adds margin for
+// the device's float evaluation of the plane and of the hit point.
+void octree_grid(const OctreeHost& t, const float bmin[3], const float bmax[3], OctGrid& g)
+{
+    const double scale = std::ldexp(1.0, t.depth);
+    float cmin = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        const double r0 = bmin[k], size = (double)bmax[k] - (double)bmin[k];
+        const double cell = size > 0.0 ? size / scale : 1.0;
+        double w = 0.0;
+        for (const OctNode& nd : t.nodes) {
+            const double v[2] = {comp(mk(nd.lo.x, nd.lo.y, nd.lo.z), k), comp(mk(nd.hi.x, nd.hi.y, nd.hi.z), k)};
+            for (double x : v) w = std::max(w, std::fabs(x - (r0 + std::nearbyint((x - r0) / cell) * cell)));
+        }
+        const float ulp = std::nextafter(std::max(std::fabs(bmin[k]), std::fabs(bmax[k])), INFINITY) -
+                          std::max(std::fabs(bmin[k]), std::fabs(bmax[k]));
+        g.r0[k] = bmin[k];
+        g.cell[k] = (float)cell;
+        g.inv_cell[k] = (float)(1.0 / cell);
+        g.band[k] = (float)(4.0 * w + 8.0 * (double)ulp);
+        cmin = std::min(cmin, (float)cell);
+    }
+    g.reach = 0.5f * cmin;
+}
+
+// Distance of x to the nearest plane of axis k, as the device evaluates it
+// (tmpt_traverse.h octree_crack), and that plane's number.
+static float plane_dist(const OctGrid& g, int k, float x, float& j)
+{
+    const float rel = x - g.r0[k];
+    j = rintf(rel * g.inv_cell[k]);
+    return fabsf(fmaf(-j, g.cell[k], rel));
+}
+
+int32_t octree_flat_triangles(const float* tris9, int32_t n, const OctGrid& g, std::vector<uint8_t>& flat)
+{
+    flat.assign((size_t)n, 0);
+    int32_t count = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        const float* v = tris9 + 9 * (size_t)i;
+        for (int k = 0; k < 3 && !flat[(size_t)i]; ++k) {
+            float j0, j1, j2;
+            const float d0 = plane_dist(g, k, v[k], j0), d1 = plane_dist(g, k, v[3 + k], j1),
+                        d2 = plane_dist(g, k, v[6 + k], j2);
+            const float lim = 2.0f * g.band[k];
+            if (j0 == j1 && j1 == j2 && d0 <= lim && d1 <= lim && d2 <= lim) flat[(size_t)i] = 1;
+        }
+        count += flat[(size_t)i];
+    }
+    return count;
+}
+
 uint64_t octree_digest(const OctreeHost& t)
 {
     uint64_t h = 1469598103934665603ull;

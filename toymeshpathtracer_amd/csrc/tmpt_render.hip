@@ -328,6 +328,7 @@ __global__ void __launch_bounds__(BLOCK) k_redo(SceneView sv, RenderArgs a, uint
     if (lane_id() == 0 && re + rs) {
         atomicAdd(&counters[0], (unsigned long long)(re + rs));
         atomicAdd(&counters[3], (unsigned long long)re);
+        atomicAdd(&counters[kRedoRaysCounter], (unsigned long long)(re + rs));
     }
 }
 
@@ -383,7 +384,9 @@ __global__ void __launch_bounds__(BLOCK) k_mega(SceneView sv, RenderArgs a,
 // with one [tmin, tmax] for all (RANGED = 0), or n x {o.xyz, d.xyz, tmin, tmax}
 // (RANGED = 1, the per-call range of scene.h:36-37).  hits n x {pos, normal, t}
 // where ids >= 0.
-template <bool ANY, bool RANGED, int BLOCK, int SL, bool SOA = false>
+// NEG: the range can start behind the origin (every per-ray range, and a
+// single range with tmin < 0): the traversal's far-distance slack by magnitude.
+template <bool ANY, bool RANGED, int BLOCK, int SL, bool SOA = false, bool NEG = RANGED>
 __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* __restrict__ rays,
                                                      int64_t n, float tmin, float tmax,
                                                      float* __restrict__ hits,
@@ -405,8 +408,8 @@ __global__ void __launch_bounds__(BLOCK) k_intersect(SceneView sv, const float* 
         if (sv.oct && !octree_root_hit(sv, o, d, t0, t1)) {
             atomicAdd(&sv.oct->ties[1], 1ull);
         } else {
-            // a per-ray range may start behind the origin: sign-aware slack (NEG)
-            id = traverse<ANY, false, BLOCK, SL, false, SOA, RANGED>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
+            // a range that may start behind the origin: sign-aware slack (NEG)
+            id = traverse<ANY, false, BLOCK, SL, false, SOA, NEG>(sv, make_trav_ray(o, d), t0, t1, t, u, v, st, cnt);
         }
         ids[i] = id;
         if (id >= 0) {
@@ -631,6 +634,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) k_wf_trace(SceneView sv, WfState 
                 active = false;
                 if (COUNT) max_steps = max(max_steps, steps);
                 if (ANY) {
+                    if (octree_flag(sv, r, ts)) settle_any(sv, r, kMinT, kMaxT, ts);  // a flat triangle, a crack
                     if (ts.best >= 0) s.light[(int64_t)(s.depth[p] - 1) * P + p] = 0.0f;
                 } else {
                     settle_closest<BLOCK, SL, TOPC, false, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
@@ -888,6 +892,11 @@ struct PathCtl {
     uint32_t redo_cap;
     uint32_t redo_inline;  // 0 (test hook, option redo_inline): no redo phase, k_redo takes every entry
     uint32_t redo_lanes;   // lanes per wave that take redo tickets (1..64)
+    // With the octree: shadow answers can need it too (a flat triangle in the
+    // scene, or the light direction can run along a crack; render_persistent
+    // decides) -- the finished shadow queries are checked as closest hits are
+    // (octree_flag), so HELP and DEFER are off then.
+    uint32_t oct_shadow;
 };
 
 constexpr uint32_t kSimdKeys = 8u * 8u * 2u * 16u * 4u;  // XCC x SE x SH x CU x SIMD (HW_ID fields)
@@ -1370,10 +1379,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             // (the row engines, SAMP >= 2, answer in the closest-hit branch
             // with the serial walk: the wave walk's registers spill there --
             // row seeding 927 -> 888 MRays/s)
+            // Also the crack queries (octree_flag), and -- where the host says a
+            // shadow answer can need it (PathCtl::oct_shadow: a flat triangle in
+            // the scene, or a light direction that can run along a crack) --
+            // finished shadow queries whose hit the reference may not see: the
+            // walk's closest answer gives their hit / miss bit.
             bool settled = false;
             if (!DEFER && SAMP < 2) {
-                const bool fin = has_pix && !in_query && !cam && !qany && !(HELP && waiting);
-                uint64_t T = wballot(fin && octree_tie(sv, ts));
+                const bool fin = has_pix && !in_query && !cam && !(HELP && waiting) && (!qany || pc.oct_shadow);
+                uint64_t T = wballot(fin && octree_flag(sv, r, ts));
                 if (T != 0) {
                     const OctView* ov = sv.oct;
                     do {
@@ -1382,9 +1396,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const f3 qo = mk(rlane(r.o.x, l), rlane(r.o.y, l), rlane(r.o.z, l));
                         const f3 qd = mk(rlane(r.d.x, l), rlane(r.d.y, l), rlane(r.d.z, l));
                         const OctHit h = octree_walk_wave(ov->nodes, ov->refs, ov->n, sv.tri_orig, qo, qd, kMinT, kMaxT,
-                                                          rlane(ts.bt, l));
+                                                          rlane(qany ? -INFINITY : ts.bt, l));
                         if (lane_id() == l) {
-                            atomicAdd(&ov->ties[0], 1ull);
+                            octree_count(ov, ts.best);
                             ts.best = h.best;
                             ts.bt = h.t;
                             ts.bu = h.u;
@@ -1416,7 +1430,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         // traced again whole by redo_sample.  It finishes at
                         // once with colour x = -1 (no path colour is negative),
                         // which the colour-buffer stores below skip.
-                        drop = octree_tie(sv, ts);
+                        drop = octree_flag(sv, r, ts);
                         if (wany(drop)) {
                             if (drop) {
                                 const unsigned long long slot = atomicAdd(&counters[kRedoCounter], 1ull);
@@ -1429,7 +1443,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         }
                         ts.best >>= 1;  // -1 stays -1
                     } else if (SAMP >= 2) {
-                        const bool tie = octree_tie(sv, ts);
+                        const bool tie = octree_flag(sv, r, ts);
                         if (wany(tie)) {
                             if (tie) settle_closest<BLOCK, SL, true, SOA, false>(sv, r, 0.0f, kMinT, kMaxT, ts, st);
                         }
@@ -1482,6 +1496,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         finish = true;
                     }
                 } else if (SAMP < 3) {  // shadow query of bounce depth-1
+                    if (SAMP == 2 && pc.oct_shadow && octree_flag(sv, r, ts))
+                        settle_any(sv, r, kMinT, kMaxT, ts);  // the row engines' serial walk (pixel, sample: above)
                     if (ts.best >= 0) light[(depth - 1) * LS] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
                         start = true;  // the scattered ray of that bounce
@@ -2564,6 +2580,22 @@ __global__ void __launch_bounds__(256) k_resolve_chains(PixelChains ch, const fl
     out[p] = pack_pixel(col, spp_recip);
 }
 
+// PathCtl::oct_shadow: whether a shadow query's answer can need the octree --
+// a triangle lying flat on one of its planes, or a light direction that can
+// drift along a crack (octree_crack's test at the smallest t a hit can have,
+// kMinT): the constant light of main.cpp:36 never can in these scenes, but
+// the test is the device's own.
+static uint32_t oct_shadow_check(const Scene& s)
+{
+    if (!s.oct_view || s.opt.tie_rule != 0) return 0u;
+    if (s.oct_flat > 0) return 1u;
+    const f3 ld = light_dir();
+    const float l[3] = {fabsf(ld.x), fabsf(ld.y), fabsf(ld.z)};
+    for (int k = 0; k < 3; ++k)
+        if (l[k] * fminf(kMinT, s.oct_grid.reach) <= 2.0f * s.oct_grid.band[k]) return 1u;
+    return 0u;
+}
+
 // Persistent path engine: one launch per frame (shard).
 int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count,
                       unsigned long long* d_counters)
@@ -2669,6 +2701,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const int64_t lanes = (int64_t)grid * kBlk;
     int help = ordered && fn == fn_default && 2 * P <= 5 * lanes ? 1 : 0;
     if (o.help >= 0) help = o.help != 0 && !count && !prof && !a.jt;
+    const uint32_t oct_shadow = oct_shadow_check(s);
+    if (oct_shadow) help = 0;  // the helpers' shadow answers are not checked
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
     if (o.pair >= 0) pair = o.pair;
     if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
@@ -2687,6 +2721,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     PathCtl pc;
     memset(&pc, 0, sizeof(pc));
     pc.heads = heads;
+    pc.oct_shadow = oct_shadow;
     pc.P = P;
     pc.nblk = nblk;
     pc.blk = blk;
@@ -2747,6 +2782,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         // 184.8 / 190.2 / 185.3, 1/2 93.1 / 96.3 / 94.9, 1/4 47.7 / 49.4 /
         // 49.8, 1/8 24.6 / 25.5 / 27.1
         const bool defer = a.jt && !count && !prof && !soa && pc.sbuf && a.root_check == 0 && o.tie_defer != 0 &&
+                           !oct_shadow &&
                            (o.tie_defer > 0 || a.slots * (int64_t)a.spp >= 192 * lanes);
         bool redo = defer && s.oct_view && o.tie_rule == 0;
         if (redo && o.redo_cap > 0 && s.redo_cap != (uint32_t)o.redo_cap) {  // the test hook's size
@@ -2812,7 +2848,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                                                                   pc.sb_sp, (uint32_t*)s.ws, d_counters);
                 TMPT_HIP(hipGetLastError());
                 TMPT_HIP(hipEventRecord(s.path_ev[1], s.stream));
-                s.path_launches = 2;
+                s.redo_launches = 1;  // timed apart from k_path (tmpt_stats.redo_ms)
             }
             break;
         }
@@ -3073,6 +3109,7 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     pc.lane_cap = 64u;
     pc.chunk = kChunk;
     pc.rs_noshadow = 1;
+    pc.oct_shadow = oct_shadow_check(s);
     pc.rss = S;
     fn4<<<grid, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, ovf, spec_ctr);
     TMPT_HIP(hipGetLastError());
@@ -3331,6 +3368,7 @@ int render_rowspec(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long
         q.pc.rs_end = q.rs_end;
         q.pc.p_dev = q.rs.total;
         q.pc.rs_noshadow = noshadow ? 1 : 0;
+        q.pc.oct_shadow = oct_shadow_check(s);
         q.rs.lpix = lpix;
         q.rs.lstate = lstate;
         q.rs.lslot = lslot;
@@ -3482,10 +3520,17 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
 {
     if (ensure_counters(s)) return -1;
     TMPT_HIP(hipMemsetAsync(s.ties, 0, 2 * sizeof(unsigned long long), s.stream));
+    TMPT_HIP(hipMemsetAsync(s.counters + kCrackCounter, 0, sizeof(unsigned long long), s.stream));
     const bool soa = s.soa.na != nullptr;
+    // one range starting behind the origin takes the NEG slack too
+    const bool neg1 = !ranged && tmin < 0.0f;
     auto fn = soa ? (ranged ? (any ? k_intersect<true, true, kBlk, kSL, true> : k_intersect<false, true, kBlk, kSL, true>)
+                    : neg1  ? (any ? k_intersect<true, false, kBlk, kSL, true, true>
+                                   : k_intersect<false, false, kBlk, kSL, true, true>)
                             : (any ? k_intersect<true, false, kBlk, kSL, true> : k_intersect<false, false, kBlk, kSL, true>))
                   : (ranged ? (any ? k_intersect<true, true, kBlk, kSL> : k_intersect<false, true, kBlk, kSL>)
+                    : neg1  ? (any ? k_intersect<true, false, kBlk, kSL, false, true>
+                                   : k_intersect<false, false, kBlk, kSL, false, true>)
                             : (any ? k_intersect<true, false, kBlk, kSL> : k_intersect<false, false, kBlk, kSL>));
     int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (n + kBlk - 1) / kBlk));
@@ -3494,6 +3539,8 @@ int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float 
     fn<<<grid, kBlk, 0, s.stream>>>(view(s), d_rays, n, tmin, tmax, d_hits, d_ids, (uint32_t*)s.ws);
     TMPT_HIP(hipGetLastError());
     TMPT_HIP(hipMemcpyAsync(s.counters_host + kTieCounter, s.ties, 2 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, s.stream));
+    TMPT_HIP(hipMemcpyAsync(s.counters_host + kCrackCounter, s.counters + kCrackCounter, sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s.stream));
     return 0;
 }
@@ -3597,6 +3644,9 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.chain_pixels = 0;
     s.redo_samples = 0;
     s.redo_late = 0;
+    s.redo_launches = 0;
+    s.redo_ms = 0.0;
+    s.redo_rays = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);
@@ -3633,6 +3683,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.render_ms = ms;
     s.tie_queries = c[kTieCounter];
     s.root_misses = c[kTieCounter + 1];
+    s.crack_queries = c[kCrackCounter];
 #ifdef TMPT_EXP_WALKSTAT
     {
         unsigned long long w[4] = {0, 0, 0, 0};
@@ -3652,6 +3703,12 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
         (void)hipEventElapsedTime(&k1, s.path_ev[2], s.path_ev[3]);
         if (s.path_launches == 2) (void)hipEventElapsedTime(&k0, s.path_ev[0], s.path_ev[1]);
         s.extend_ms = (double)k0 + (double)k1;
+        if (s.redo_launches) {  // the k_redo launch after the main one: its own figure
+            float kr = 0.0f;
+            (void)hipEventElapsedTime(&kr, s.path_ev[0], s.path_ev[1]);
+            s.redo_ms = kr;
+            s.redo_rays = c[kRedoRaysCounter];
+        }
         s.extend_rays = c[3];
         s.shadow_rays = c[0] - c[3];
         s.node_visits = c[1];

@@ -508,28 +508,77 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
     return h.best;
 }
 
-// Whether a finished closest-hit query is a flagged tie the octree answers.
-__device__ __forceinline__ bool octree_tie(const SceneView& sv, const TravState& ts)
+// Whether a hit at t on the ray (o, d) may lie in one of the octree's cracks
+// (tmpt_internal.h OctGrid): for some axis k the hit point is within band[k]
+// of a plane of the octree's finest grid and the ray drifted less than
+// 2 band[k] along k over min(t, reach) -- it ran along that plane, where a
+// gap between two subtrees' boxes can hide the leaves that hold the triangle
+// from the reference's walk.  The plane distance is evaluated as the host's
+// flat-triangle test evaluates it (tmpt_octree.cpp plane_dist).
+TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
 {
-    return sv.oct != nullptr && ts.best >= 0 && (ts.best & 1) != 0;
+    const float oc[3] = {o.x, o.y, o.z}, dc[3] = {d.x, d.y, d.z};
+    const float span = fminf(t, g.reach);
+    bool f = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (fabsf(dc[k]) * span <= 2.0f * g.band[k]) {
+            const float rel = fmaf(t, dc[k], oc[k]) - g.r0[k];
+            const float j = rintf(rel * g.inv_cell[k]);
+            f |= fabsf(fmaf(-j, g.cell[k], rel)) <= g.band[k];
+        }
+    }
+    return f;
+}
+
+// Whether a finished query is one the octree answers: bit 0 of TravState::best
+// (a tie on t, or a triangle lying flat on an octree plane -- its record's
+// index is odd) or a hit that may lie in a crack.  The any-hit query's bit 0
+// can only come from a flat triangle (it stops at its first accept).
+__device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& r, const TravState& ts)
+{
+    if (sv.oct == nullptr || ts.best < 0) return false;
+    return (ts.best & 1) != 0 || octree_crack(sv.oct->grid, r.o, r.d, ts.bt);
+}
+
+// counts a query octree_flag sent to the octree: ties[0] (bit 0) or ties[6] (crack)
+__device__ __forceinline__ void octree_count(const OctView* ov, int best)
+{
+    atomicAdd(&ov->ties[(best & 1) ? 0 : 6], 1ull);
 }
 
 // A finished closest-hit query: the triangle index from TravState::best; a
-// flagged tie is answered again over the octree (the reference's pick among
-// the tied triangles, and its whole answer for that ray); without an octree
-// the lowest index stands.  (The walk stops at the first triangle at the tied
-// t, which is the reference's answer: nothing lies nearer.)
+// flagged query is answered again over the octree (the reference's pick among
+// tied triangles, its whole answer for that ray); without an octree the
+// lowest index stands.  (The walk stops at the first triangle at the BVH's
+// closest t, which is the reference's answer when it reaches it: nothing lies
+// nearer.)
 template <int BLOCK, int SL, bool TOPC, bool SOA, bool NEG>
 __device__ __forceinline__ void settle_closest(const SceneView& sv, const TravRay& r, float tlo, float tmin,
                                                float tmax, TravState& ts, TravStack<BLOCK, SL>& st)
 {
     (void)tlo;
     (void)st;
-    if (octree_tie(sv, ts)) {
-        atomicAdd(&sv.oct->ties[0], 1ull);
+    if (octree_flag(sv, r, ts)) {
+        octree_count(sv.oct, ts.best);
         ts.best = octree_closest(sv, r.o, r.d, tmin, tmax, ts.bt, ts.bt, ts.bu, ts.bv);
     } else {
         ts.best >>= 1;  // -1 stays -1
+    }
+}
+
+// A finished any-hit query (the shadow ray's hit / miss bit): a hit the
+// reference's octree might not see (a flat triangle, a crack) is answered by
+// its walk; otherwise the first accepted triangle stands.
+__device__ __forceinline__ void settle_any(const SceneView& sv, const TravRay& r, float tmin, float tmax,
+                                           TravState& ts)
+{
+    if (octree_flag(sv, r, ts)) {
+        octree_count(sv.oct, ts.best);
+        float t, u, v;
+        ts.best = octree_closest(sv, r.o, r.d, tmin, tmax, -INFINITY, t, u, v);
+    } else {
+        ts.best >>= 1;  // the doubled index of the first accepted triangle (-1 stays -1)
     }
 }
 
@@ -561,7 +610,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
         while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA, NEG>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
         if (!ANY) settle_closest<BLOCK, SL, TOPC, SOA, NEG>(sv, r, tlo, tmin, tmax, ts, st);
-        else ts.best >>= 1;  // the doubled index of the first accepted triangle (-1 stays -1)
+        else settle_any(sv, r, tmin, tmax, ts);
     }
     bt = ts.bt;
     bu = ts.bu;
