@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liboracle.so")
+# ORACLE_LIB: another build of it (tools/san_check.sh: the sanitizer build, build_san/)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 
 ACCEL_OCTREE, ACCEL_BVH, ACCEL_LINEAR = 0, 1, 2
 TIE_VISIT, TIE_INDEX = 0, 1

@@ -431,7 +431,7 @@ static void oct_push_tris(orc_scene* s, const int32_t* ids, int32_t cnt, int64_t
             s->cap_oct_tris = s->cap_oct_tris ? s->cap_oct_tris * 2 : 4096;
         s->oct_tris = (int32_t*)realloc(s->oct_tris, (size_t)s->cap_oct_tris * sizeof(int32_t));
     }
-    memcpy(s->oct_tris + s->n_oct_tris, ids, (size_t)cnt * sizeof(int32_t));
+    if (cnt > 0) memcpy(s->oct_tris + s->n_oct_tris, ids, (size_t)cnt * sizeof(int32_t)); /* (UBSan: no NULL to memcpy) */
     s->oct[node].tri_off = (int32_t)s->n_oct_tris;
     s->oct[node].tri_cnt = cnt;
     s->n_oct_tris += cnt;

@@ -916,6 +916,9 @@ def test_tie_defer_same_frame_and_rays(gpu, sponza_path, shards):
         st1 = sc.stats()
         assert st1.redo_samples > 0
         assert st1.tie_queries == st0.tie_queries  # the redo pass meets the same ties
+        # the list entries are written through to memory (sc1): every listed
+        # sample is visible to the waiting lanes at once, so none is left late
+        assert st1.redo_late == 0 and st1.redo_launches == 0
         assert rays == rays_exact and np.array_equal(img, exact)
         sc.set_option("redo_cap", 1)
         img2, rays2 = sc.trace_image(cam, w, h, spp, **kw)
@@ -924,7 +927,9 @@ def test_tie_defer_same_frame_and_rays(gpu, sponza_path, shards):
         sc.set_option("redo_cap", 0)
         sc.set_option("redo_inline", 0)  # every dropped sample to the k_redo launch
         img3, rays3 = sc.trace_image(cam, w, h, spp, **kw)
-        assert sc.stats().redo_samples == st1.redo_samples
+        st3 = sc.stats()
+        assert st3.redo_samples == st1.redo_samples
+        assert st3.redo_launches == 1 and st3.redo_late == st1.redo_samples and st3.redo_rays > 0
         assert rays3 == rays_exact and np.array_equal(img3, exact)
     if shards == 1:
         ref, _ = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE,

@@ -1,0 +1,63 @@
+"""Same-box A/B of k_path time: the package under test (default: this tree)
+against another build of it (a directory holding toymeshpathtracer_amd/, e.g.
+tools/_bin/base from an earlier commit), alternating, on the bench frame.
+
+  python tools/ab_kpath.py <pkgdir_a> <pkgdir_b> [frames] [loads]
+  loads: comma list of seed:shards, e.g. sample:1,sample:8,pixel:1
+Prints per load the median k_path ms (tmpt_stats.extend_ms) of each build."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import sys, os, json, statistics
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[2], "data"))
+import toymeshpathtracer_amd as tm
+import gen_standin_sponza
+frames = int(sys.argv[3]); loads = sys.argv[4].split(",")
+tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
+w, h, spp = 1920, 1080, 64
+cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL}
+out = {}
+with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+    for ld in loads:
+        sd, n = ld.split(":"); n = int(n)
+        ms = []
+        for i in range(frames + 1):
+            sc.trace_image(cam, w, h, spp, seed_mode=seeds[sd], band_rows=1, shard=n - 1, num_shards=n)
+            if i: ms.append(sc.stats().extend_ms)
+        out[ld] = statistics.median(ms)
+print(json.dumps(out))
+'''
+
+
+def run(pkg, frames, loads):
+    r = subprocess.run([sys.executable, "-c", CHILD, pkg, ROOT, str(frames), loads], capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode:
+        raise SystemExit(r.stderr)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def main():
+    a, b = sys.argv[1], sys.argv[2]
+    frames = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    loads = sys.argv[4] if len(sys.argv) > 4 else "sample:1,sample:8,pixel:1,pixel:8"
+    res = {a: [], b: []}
+    for rep in range(2):  # A B A B
+        for p in (a, b):
+            res[p].append(run(p, frames, loads))
+            print(p, res[p][-1], flush=True)
+    for ld in loads.split(","):
+        ma = min(r[ld] for r in res[a])
+        mb = min(r[ld] for r in res[b])
+        print(f"{ld}: {os.path.basename(a.rstrip('/')) or a} {ma:.2f} ms, {os.path.basename(b.rstrip('/')) or b} {mb:.2f} ms,"
+              f" {100 * (mb / ma - 1):+.2f} %", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -56,7 +56,10 @@ if not os.path.exists(lib_path):
 # libtmpt bind to the runtime torch already loaded, so torch CUDA tensors,
 # torch.distributed (RCCL) and our kernels share one device context.  Without
 # torch, the system ROCm runtime is used.
+# (TMPT_NO_TORCH=1: not even that -- the host sanitizer runs, tools/san_check.sh)
 try:  # pragma: no cover - depends on the environment
+    if os.environ.get("TMPT_NO_TORCH") == "1":
+        raise ImportError("TMPT_NO_TORCH")
     import torch  # noqa: F401
 except Exception:  # torch is optional for the C ABI itself
     torch = None

@@ -294,6 +294,12 @@ __device__ __forceinline__ uint2 redo_load(const uint2* p)
     return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
 }
 
+__device__ __forceinline__ void redo_put(uint2* p, uint32_t pix, uint32_t smp)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)smp << 32) | pix, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void redo_mark(uint2* p)
 {
     __hip_atomic_store(reinterpret_cast<unsigned int*>(p), kRedoDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1434,7 +1440,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         if (wany(drop)) {
                             if (drop) {
                                 const unsigned long long slot = atomicAdd(&counters[kRedoCounter], 1ull);
-                                if (slot < (unsigned long long)pc.redo_cap) pc.redo[slot] = make_uint2(pix, smp);
+                                // write-through (sc1): a plain store would sit in this
+                                // XCD's L2, unseen by a waiting lane on another XCD
+                                // until evicted, and its write-back at the kernel's end
+                                // could land after that lane's done-mark and undo it
+                                // (k_redo then traced the sample again: rays counted
+                                // twice -- MI355X_MICROARCH.md, per-XCD L2s)
+                                if (slot < (unsigned long long)pc.redo_cap) redo_put(pc.redo + slot, pix, smp);
                                 rays_e -= depth + 1u;
                                 rays_s -= depth;
                                 depth = 0;
