@@ -86,7 +86,7 @@ typedef struct {
     int32_t shard, num_shards;
     int32_t engine;
     int32_t flags;
-    /* Progressive spp (persistent engine, pixel mode): this call runs samples
+    /* Progressive spp (persistent engine, pixel or sample seeding): this call runs samples
      * [spp_begin, spp_begin + spp_count) of every pixel (spp_count 0 = to spp).
      * A call with spp_begin > 0 continues the per-pixel state (RNG, colour sum)
      * the previous call on this scene left for the same shard, so the passes
@@ -261,7 +261,7 @@ int tmpt_scene_get_option(const tmpt_scene* scene, const char* key, double* valu
  * octree (a caller's wait_stream is not waited on). */
 int tmpt_scene_build_octree(tmpt_scene* scene, const float bmin[3], const float bmax[3]);
 /* The root box main.cpp:312 gives BuildOctree: sceneMin - extra, sceneMax + extra
- * with extra = (sceneMax - sceneMin) * 0.7 (main.cpp:294-295); bmin / bmax
+ * with extra = (sceneMax - sceneMin) * 0.7 (main.cpp:296-297); bmin / bmax
  * are tmpt_load_obj's OBJ bounds.  box = {min.xyz, max.xyz}. */
 int tmpt_octree_bounds(const float bmin[3], const float bmax[3], float box[6]);
 /* Check hook (host only, no device): the octree tmpt_scene_build_octree would

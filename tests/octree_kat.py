@@ -229,7 +229,7 @@ def classify(tris, bmin, bmax, rays, t_min=0.001, t_max=1.0e7, osc=None):
 
 def grid_scene(k=3, n=6, seed=0):
     """A synthetic scene on the octree's split planes: OBJ bounds +-s with
-    s = 1/2.4 give the root box +-1 (main.cpp:294-296,312: bounds +- 0.7 x
+    s = 1/2.4 give the root box +-1 (main.cpp:296-297,312: bounds +- 0.7 x
     size), whose planes are the multiples of 1/2^j; axis-aligned quads on the
     planes c = i / 2^k and triangles with vertices snapped to them.
     Returns (tris, bmin, bmax)."""
@@ -251,7 +251,7 @@ def grid_scene(k=3, n=6, seed=0):
     for _ in range(n * 20):
         tris.append(rng.choice(planes, (3, 3)))
     tris = np.array(tris, np.float32)
-    # bounds exactly +-s so that the root box lands on +-1 (main.cpp:294-296,312)
+    # bounds exactly +-s so that the root box lands on +-1 (main.cpp:296-297,312)
     tris[0, 0] = [-s, -s, -s]
     tris[1, 0] = [s, s, s]
     bmin = tris.reshape(-1, 3).min(0)

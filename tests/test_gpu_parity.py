@@ -566,22 +566,54 @@ def test_count_visits_instrumentation(gpu):
 
 
 # ---------------------------------------------------------------- progressive spp
+@pytest.mark.parametrize("seed", [tm.SEED_PIXEL, tm.SEED_SAMPLE])
 @pytest.mark.parametrize("name,w,h,spp,passes", [("suzanne.obj", 160, 90, 16, [1, 3, 4, 8]),
-                                                 ("teapot.obj", 320, 180, 8, [5, 3])])
-def test_progressive_passes_equal_full_render(gpu, name, w, h, spp, passes):
-    """Passes of spp_count samples continue each pixel's RNG stream and colour sum:
-    the last pass is the full render bit for bit, every preview equals a full
-    render at that sample count, and the passes' rays sum to the full count."""
-    tris, bmin, bmax, sc = _scene(name)
+                                                 ("teapot.obj", 320, 180, 8, [5, 3]),
+                                                 ("teapot.obj", 96, 54, 64, [6, 2, 24, 32])])
+def test_progressive_passes_equal_full_render(gpu, name, w, h, spp, passes, seed):
+    """Passes of spp_count samples continue each pixel's RNG stream (pixel
+    seeding) or start its samples where sample seeding puts them, and carry
+    its colour sum: the last pass is the full render bit for bit, every
+    preview equals a full render at that sample count, and the passes' rays
+    sum to the full count.  Sample seeding: passes starting at odd and even
+    samples (block sizes 1, 2, 8), small frames where a pass is one block per
+    pixel; the octree built (the reference's answers, deferred ties)."""
+    tris, bmin, bmax, sc = _scene(name, octree=seed == tm.SEED_SAMPLE)
     cam = tm.Camera.for_scene(bmin, bmax, w, h)
-    full, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_PIXEL)
+    full, rays = sc.trace_image(cam, w, h, spp, seed_mode=seed)
     total = 0
-    for done, img, r in sc.trace_progressive(cam, w, h, spp, passes):
+    for done, img, r in sc.trace_progressive(cam, w, h, spp, passes, seed_mode=seed):
         total += r
-        ref, _ = sc.trace_image(cam, w, h, done, seed_mode=tm.SEED_PIXEL)
+        ref, _ = sc.trace_image(cam, w, h, done, seed_mode=seed)
         assert np.array_equal(img, ref), done
     assert np.array_equal(img, full) and total == rays
+    if seed == tm.SEED_SAMPLE:
+        ref, ref_rays = _ref_oracle(tris, bmin, bmax).render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+        assert ref_rays == rays and np.array_equal(full, ref)
     sc.close()
+
+
+def test_progressive_sample_seeding_shards_and_blocks(gpu, sponza_path):
+    """Sample seeding progressive on the bench frame's 1/8 shard (1-row bands,
+    the per-rank load at 8 GPUs) at 64 spp in passes of 8, 24, 32 and with
+    every block size of the persistent engine forced (option sample_block):
+    the last pass equals the one-call shard, which equals those rows of the
+    full frame."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 1920, 1080, 64
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    kw = dict(band_rows=1, shard=3, num_shards=8)
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        one, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, **kw)
+        for blk in (0, 1, 4):
+            sc.set_option("sample_block", blk)
+            total = 0
+            for done, img, r in sc.trace_progressive(cam, w, h, spp, [8, 24, 32], seed_mode=tm.SEED_SAMPLE, **kw):
+                total += r
+            assert total == rays and np.array_equal(img, one), blk
+        sc.set_option("sample_block", 0)
+        full, _ = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
+    assert np.array_equal(one, full[3::8])
 
 
 def test_progressive_shards_and_errors(gpu):
@@ -833,7 +865,7 @@ def test_sample_mode_shards_and_sizes(gpu, monkeypatch):
         ref, rr = osc.render(c2.as_array(), ww, hh, ss, seed_mode=oracle.SEED_SAMPLE)
         assert r == rr and np.array_equal(img, ref), (ww, hh, ss)
     with pytest.raises(tm.TmptError, match="progressive"):
-        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, spp_begin=0, spp_count=2)
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_ROW, spp_begin=0, spp_count=2)
     sc.close()
 
 

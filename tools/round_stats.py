@@ -19,7 +19,7 @@ cam = tm.Camera.for_scene(bmin, bmax, 1920, 1080, is_sponza=True)
 variants = sys.argv[3].split(";") if len(sys.argv) > 3 else None
 runs = [("pixel", tm.SEED_PIXEL, ""), ("sample", tm.SEED_SAMPLE, "")] if variants is None else \
     [("sample " + v, tm.SEED_SAMPLE, v) for v in variants]
-with tm.Scene(tris) as sc:
+with tm.Scene(tris, bounds=(bmin, bmax)) as sc:  # the product configuration (reference octree)
     defaults = {}
     for name, seed, v in runs:
         for k, val in defaults.items():

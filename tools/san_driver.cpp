@@ -87,7 +87,7 @@ int main(int argc, char** argv)
         // ---- the reference's octree on 8 threads vs the oracle's
         const float bmin[3] = {lo1.x, lo1.y, lo1.z}, bmax[3] = {hi1.x, hi1.y, hi1.z};
         float omin[3], omax[3];
-        for (int k = 0; k < 3; ++k) {  // main.cpp:294-296,312
+        for (int k = 0; k < 3; ++k) {  // main.cpp:296-297,312
             const float e = (bmax[k] - bmin[k]) * 0.7f;
             omin[k] = bmin[k] - e;
             omax[k] = bmax[k] + e;

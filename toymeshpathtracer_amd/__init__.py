@@ -215,7 +215,7 @@ def load_scene(path: str) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
 def octree_bounds(bmin, bmax) -> Tuple[np.ndarray, np.ndarray]:
     """The root box main.cpp:312 gives BuildOctree for a scene whose OBJ bounds
     are (bmin, bmax): bmin - extra, bmax + extra, extra = 0.7 x the size
-    (main.cpp:294-295), in float32."""
+    (main.cpp:296-297), in float32."""
     lo, hi = np.asarray(bmin, np.float32), np.asarray(bmax, np.float32)
     box = np.zeros(6, np.float32)
     _check(_octree_bounds(_fp(lo), _fp(hi), _fp(box)), "octree_bounds")
@@ -494,7 +494,7 @@ class Scene:
         ordering).  The call returns once
         the frame is complete on the device.
         ``spp_begin``/``spp_count``: one progressive pass (persistent engine,
-        pixel seeding) -- see :meth:`trace_progressive`."""
+        pixel or sample seeding) -- see :meth:`trace_progressive`."""
         if out is None:
             ws = None
         elif isinstance(wait_stream, str):
@@ -517,17 +517,18 @@ class Scene:
         return img, int(rays.value)
 
     def trace_progressive(self, camera: Camera, width: int, height: int, spp: int, passes,
-                          band_rows: int = 0, shard: int = 0, num_shards: int = 1):
+                          band_rows: int = 0, shard: int = 0, num_shards: int = 1, seed_mode: int = SEED_PIXEL):
         """Progressive spp: yields (samples_done, preview rgba, rays of the pass) per
         pass; ``passes`` = samples per pass (int) or a list of them summing to spp.
-        The last preview is the final image, bit-identical to one full render."""
+        The last preview is the final image, bit-identical to one full render;
+        pixel or sample seeding (the samples of a pass run side by side there)."""
         if isinstance(passes, int):
             passes = [min(passes, spp - b) for b in range(0, spp, passes)]
         if sum(passes) != spp or min(passes) < 1:
             raise ValueError("passes must be positive and sum to spp")
         done = 0
         for n in passes:
-            img, rays = self.trace_image(camera, width, height, spp, seed_mode=SEED_PIXEL,
+            img, rays = self.trace_image(camera, width, height, spp, seed_mode=seed_mode,
                                          engine=ENGINE_PERSISTENT, band_rows=band_rows, shard=shard,
                                          num_shards=num_shards, spp_begin=done, spp_count=n)
             done += n

@@ -504,7 +504,7 @@ int tmpt_octree_bounds(const float bmin[3], const float bmax[3], float box[6])
 {
     if (!bmin || !bmax || !box) return bad("tmpt_octree_bounds: null argument");
     const f3 lo = mk(bmin[0], bmin[1], bmin[2]), hi = mk(bmax[0], bmax[1], bmax[2]);
-    const f3 extra = (hi - lo) * 0.7f;  // main.cpp:294-295
+    const f3 extra = (hi - lo) * 0.7f;  // main.cpp:296-297
     const f3 a = lo - extra, b = hi + extra;  // main.cpp:312
     box[0] = a.x, box[1] = a.y, box[2] = a.z, box[3] = b.x, box[4] = b.y, box[5] = b.z;
     return 0;
@@ -672,8 +672,8 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
         d->spp_count > d->spp - d->spp_begin)
         return bad("tmpt_render: invalid spp_begin / spp_count");
     const bool progressive = d->spp_begin > 0 || (d->spp_count > 0 && d->spp_count < d->spp);
-    if (progressive && (d->engine != TMPT_ENGINE_PERSISTENT || d->seed_mode != TMPT_SEED_PIXEL))
-        return bad("tmpt_render: progressive spp needs the persistent engine and pixel seeding");
+    if (progressive && (d->engine != TMPT_ENGINE_PERSISTENT || d->seed_mode == TMPT_SEED_ROW))
+        return bad("tmpt_render: progressive spp needs the persistent engine and pixel or sample seeding");
     (void)hipGetLastError();  // clear a stale error of an earlier failed call (launch checks read it)
     Scene& s = h->s;
     TMPT_HIP(hipSetDevice(s.device));

@@ -81,7 +81,7 @@ int main(int argc, const char** argv)
     double dt = 0.0;
     const double t0 = now_s();
     // scene builds + renders; tmpt_render_multi times the renders alone (main.cpp:319-333)
-    // BuildOctree(sceneMin - extra, sceneMax + extra), main.cpp:294-296, 312
+    // BuildOctree(sceneMin - extra, sceneMax + extra), main.cpp:296-297, 312
     float box[6];
     tmpt_octree_bounds(bmin, bmax, box);
     if (tmpt_render_multi(tris, n, box, &cam, &desc, devs.data(), gpus, image.data(), &total, &dt)) {

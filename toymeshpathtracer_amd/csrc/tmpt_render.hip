@@ -869,6 +869,7 @@ struct PathCtl {
     // units).  With nblk > 1 each sample's colour goes to sbuf[s * slots + pixel]
     // and k_resolve sums them in sample order (main.cpp:218's col += Trace).
     uint32_t nblk, blk;
+    uint32_t blk0;  // progressive pass: the block of its first sample (units = the pass's blocks)
     float4* __restrict__ sbuf;
     uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp ([pixel][sample]: 1, spp)
     uint32_t pair;          // sample pairs (2k, 2k+1) of a unit written back to back (one 32-B sector)
@@ -1340,7 +1341,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     } else if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
                         const uint32_t unit = res + k;
                         pix = unit / pc.nblk;
-                        smp0 = (unit - pix * pc.nblk) * pc.blk;
+                        smp0 = (unit - pix * pc.nblk + pc.blk0) * pc.blk;  // blk0: a progressive pass's first block
                     } else {
                         pix = (kFull && pc.order) ? pc.order[res + k] : res + k;
                     }
@@ -1896,17 +1897,28 @@ __global__ void __launch_bounds__(256) k_order_keys(const uint32_t* __restrict__
 // then main.cpp:221-233.  The buffer is [pixel][sample]: one wave per 64
 // pixels stages 16 samples of each in LDS with coalesced 256-B reads (16
 // lanes per pixel run), then every lane sums its own pixel's samples in order.
+// A progressive pass (prog != null) sums its samples [s_begin, s_end) onto the
+// sum the previous pass left in prog (none when s_begin = 0), keeps the new sum
+// there, and writes the preview with out_recip = 1/s_end (the full render's
+// 1/spp on the last pass).
 __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sbuf, int64_t P, int32_t spp,
-                                                    float spp_recip, uint32_t* __restrict__ out)
+                                                    float spp_recip, uint32_t* __restrict__ out,
+                                                    int32_t s_begin = 0, int32_t s_end = -1,
+                                                    float4* __restrict__ prog = nullptr)
 {
     constexpr int kC = 16;                  // samples per staged chunk
     __shared__ float4 tile[64][kC + 1];     // +1: a lane's row starts on another bank
     const int64_t p0 = (int64_t)blockIdx.x * 64;
     const int t = threadIdx.x;
     const int np = (int)min<int64_t>(64, P - p0);
+    if (s_end < 0) s_end = spp;
     f3 col = mk(0.0f, 0.0f, 0.0f);
-    for (int32_t s0 = 0; s0 < spp; s0 += kC) {
-        const int nc = min(kC, spp - s0);
+    if (prog && s_begin > 0 && t < np) {
+        const float4 c = prog[p0 + t];
+        col = mk(c.x, c.y, c.z);
+    }
+    for (int32_t s0 = s_begin; s0 < s_end; s0 += kC) {
+        const int nc = min(kC, s_end - s0);
         for (int e = t; e < 64 * kC; e += 64) {
             const int i = e / kC, j = e - i * kC;
             if (i < np && j < nc) tile[i][j] = sbuf[(size_t)(p0 + i) * (size_t)spp + (size_t)(s0 + j)];
@@ -1916,7 +1928,10 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
             for (int j = 0; j < nc; ++j) col = col + mk(tile[t][j].x, tile[t][j].y, tile[t][j].z);
         __syncthreads();
     }
-    if (t < np) out[p0 + t] = pack_pixel(col, spp_recip);
+    if (t < np) {
+        if (prog) prog[p0 + t] = make_float4(col.x, col.y, col.z, 0.0f);
+        out[p0 + t] = pack_pixel(col, spp_recip);
+    }
 }
 
 // ============================================================ speculative row seeding
@@ -2659,28 +2674,43 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // 113.3/110.9/110.2/111.7; 1/4 blk 1/2/4 = 57.1/56.2/56.6; 1/8 blk 1/2/4/8
     // = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane, so 60 picks 8, 4,
     // 2, 1 at N = 1, 2, 4, 8.  Option sample_block fixes it.
-    uint32_t blk = 1u, nblk = 1u;
+    uint32_t blk = 1u, nblk = 1u, blk0 = 0u;
+    // Progressive passes in sample seeding (samples [s0, s1) of every pixel):
+    // the units are the blocks of the pass -- a block size that divides s0, so
+    // the blocks keep their alignment -- and every sample's colour goes to the
+    // colour buffer; k_resolve_px adds the pass's samples, in order, to the sum
+    // the previous pass left (main.cpp:218 summed across the passes).
+    const bool pass = a.jt && (a.smp_begin > 0 || a.smp_end < a.spp);
+    const int64_t s0 = a.smp_begin, s1 = a.smp_end;
     if (a.jt) {
         constexpr int64_t kUnitsPerLane = 60;
         const int64_t lanes0 = (int64_t)grid * kBlk;
         blk = 1u;
-        while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)a.spp &&
-               a.slots * (((int64_t)a.spp + blk * 2 - 1) / (blk * 2)) >= kUnitsPerLane * lanes0)
+        while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)(s1 - s0) &&
+               a.slots * ((s1 - s0 + blk * 2 - 1) / (blk * 2)) >= kUnitsPerLane * lanes0)
             blk *= 2u;
         if (o.sample_block > 0) blk = (uint32_t)o.sample_block;
-        while (a.slots * (((int64_t)a.spp + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
-        nblk = (uint32_t)(((int64_t)a.spp + blk - 1) / blk);
+        while (a.slots * ((s1 - s0 + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
+        while (s0 % blk) blk /= 2u;  // a pass's first sample starts a block
+        blk0 = (uint32_t)(s0 / blk);
+        nblk = (uint32_t)((s1 + blk - 1) / blk - blk0);
         // Several blocks per pixel need the per-sample colour buffer (16 B per
         // sample of the tile: 2.1 GB at 1080p x 64).  If it does not fit in 3/4
         // of the free device memory (or the sbuf_max option), the pixel is one
-        // unit: same image, only the tail of a small shard is longer.
-        if (nblk > 1) {
+        // unit: same image, only the tail of a small shard is longer.  A
+        // progressive pass needs the buffer whatever its block count.
+        if (nblk > 1 || pass) {
             const size_t need = sizeof(float4) * (size_t)a.spp * (size_t)a.slots;
             size_t fr = 0, tot = 0;
             size_t budget = hipMemGetInfo(&fr, &tot) == hipSuccess ? fr / 4 * 3 : 0;
             budget += s.sbuf_bytes;  // the buffer already held is free for this call
             if (o.sbuf_max > 0.0) budget = std::min(budget, (size_t)o.sbuf_max);
             if (need > budget) {
+                if (pass) {
+                    set_error("tmpt_render: progressive passes in sample seeding need the per-sample colour buffer (" +
+                              std::to_string(need >> 20) + " MiB), which does not fit: render the frame in one call");
+                    return -12;
+                }
                 while (blk < (uint32_t)a.spp) blk *= 2u;
                 nblk = 1u;
             }
@@ -2737,10 +2767,11 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.P = P;
     pc.nblk = nblk;
     pc.blk = blk;
+    pc.blk0 = blk0;
     RenderArgs as = a;  // sample seeding: a lane's run of samples is its block
     if (a.jt) {
         as.bmask = nblk > 1 ? blk - 1u : 2047u;
-        if (nblk > 1) {
+        if (nblk > 1 || pass) {
             const size_t need = sizeof(float4) * (size_t)a.spp * (size_t)a.slots;
             if (s.sbuf_bytes < need) {
                 if (s.sbuf) (void)hipFree(s.sbuf);
@@ -2865,8 +2896,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             break;
         }
         if (pc.sbuf) {
-            k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(pc.sbuf, a.slots, a.spp,
-                                                                             a.spp_recip, d_out);
+            k_resolve_px<<<(unsigned)((a.slots + 63) / 64), 64, 0, s.stream>>>(
+                pc.sbuf, a.slots, a.spp, a.out_recip, d_out, a.smp_begin, a.smp_end, pass ? a.prog : nullptr);
             TMPT_HIP(hipGetLastError());
         }
         return 0;
