@@ -2,7 +2,8 @@
 against another build of it (a directory holding toymeshpathtracer_amd/, e.g.
 tools/_bin/base from an earlier commit), alternating, on the bench frame.
 
-  python tools/ab_kpath.py <pkgdir_a> <pkgdir_b> [frames] [loads]
+  python tools/ab_kpath.py <pkgdir_a>[:opts],<pkgdir_b>[:opts][,...] [frames] [loads]
+  opts: scene build options with ';' between them, e.g. .:split=20;leaf_max=4
   loads: comma list of seed:shards, e.g. sample:1,sample:8,pixel:1
 Prints per load the median k_path ms (tmpt_stats.extend_ms) of each build."""
 import json
@@ -14,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r'''
 import sys, os, json, statistics
-sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[2], "data"))
+pkg, _, opts = sys.argv[1].partition(":")  # <package dir>[:<scene options>]
+sys.path.insert(0, pkg); sys.path.insert(0, os.path.join(sys.argv[2], "data"))
 import toymeshpathtracer_amd as tm
 import gen_standin_sponza
 frames = int(sys.argv[3]); loads = sys.argv[4].split(",")
@@ -23,7 +25,7 @@ w, h, spp = 1920, 1080, 64
 cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
 seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL}
 out = {}
-with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+with tm.Scene(tris, bounds=(bmin, bmax), options=opts.replace(";", ",") or None) as sc:
     for ld in loads:
         sd, n = ld.split(":"); n = int(n)
         ms = []
@@ -44,19 +46,21 @@ def run(pkg, frames, loads):
 
 
 def main():
-    a, b = sys.argv[1], sys.argv[2]
-    frames = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    loads = sys.argv[4] if len(sys.argv) > 4 else "sample:1,sample:8,pixel:1,pixel:8"
-    res = {a: [], b: []}
-    for rep in range(2):  # A B A B
-        for p in (a, b):
+    pkgs = sys.argv[1].split(",")  # the first is the reference of the comparison
+    frames = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    loads = sys.argv[3] if len(sys.argv) > 3 else "sample:1,sample:8,pixel:1,pixel:8"
+    res = {p: [] for p in pkgs}
+    for rep in range(2):  # A B C .. A B C ..
+        for p in pkgs:
             res[p].append(run(p, frames, loads))
-            print(p, res[p][-1], flush=True)
+            print(p, {k: round(v, 3) for k, v in res[p][-1].items()}, flush=True)
     for ld in loads.split(","):
-        ma = min(r[ld] for r in res[a])
-        mb = min(r[ld] for r in res[b])
-        print(f"{ld}: {os.path.basename(a.rstrip('/')) or a} {ma:.2f} ms, {os.path.basename(b.rstrip('/')) or b} {mb:.2f} ms,"
-              f" {100 * (mb / ma - 1):+.2f} %", flush=True)
+        base = min(r[ld] for r in res[pkgs[0]])
+        line = [f"{ld}: {pkgs[0]} {base:.2f} ms"]
+        for p in pkgs[1:]:
+            m = min(r[ld] for r in res[p])
+            line.append(f"{p} {m:.2f} ms ({100 * (m / base - 1):+.2f} %)")
+        print(", ".join(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -239,6 +239,7 @@ void octree_grid(const OctreeHost& t, const float bmin[3], const float bmax[3], 
         g.cell[k] = (float)cell;
         g.inv_cell[k] = (float)(1.0 / cell);
         g.band[k] = (float)(4.0 * w + 8.0 * (double)ulp);
+        g.drift[k] = 2.0f * g.band[k];
         cmin = std::min(cmin, (float)cell);
     }
     g.reach = 0.5f * cmin;

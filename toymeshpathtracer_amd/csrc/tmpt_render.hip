@@ -116,16 +116,20 @@ __device__ __forceinline__ void flush_counts(unsigned long long* counters, uint3
 // ============================================================ megakernel
 // Whole query; TOPC: the top BVH4 levels from the block's LDS copy (the
 // latency-bound row chains).
-template <bool ANY, bool COUNT, bool TOPC, int BLOCK, int SL>
+template <bool ANY, bool COUNT, bool TOPC, int BLOCK, int SL, bool CHECK_ANY = true>
 __device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float& t, float& u, float& v,
                                           TravStack<BLOCK, SL>& st, TravCount& cnt)
 {
-    return traverse<ANY, COUNT, BLOCK, SL, TOPC>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u, v, st, cnt);
+    return traverse<ANY, COUNT, BLOCK, SL, TOPC, false, false, CHECK_ANY>(sv, make_trav_ray(o, d), kMinT, kMaxT, t, u,
+                                                                          v, st, cnt);
 }
 
 // rays: closest-hit queries, srays: shadow queries (the same counter where the
 // caller does not split them)
-template <bool COUNT, int BLOCK, int SL, bool TOPC = false>
+// CHECK_ANY: the shadow answers are checked against the octree (settle_any);
+// the deferred-tie redo passes false (tie_defer is off wherever a shadow
+// answer can need the octree, PathCtl::oct_shadow)
+template <bool COUNT, int BLOCK, int SL, bool TOPC = false, bool CHECK_ANY = true>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, uint32_t& srays, TravStack<BLOCK, SL>& st, float* lbuf,
                                          TravCount& cnt, bool root_check)
@@ -148,7 +152,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32
             float lc = light_cosine(nrm, d);
             if (lc > 0.0f) {  // a zero light term does not depend on the answer
                 float ts, us, vs;
-                int sid = mega_query<true, COUNT, TOPC>(sv, pos, light_dir(), ts, us, vs, st, cnt);
+                int sid = mega_query<true, COUNT, TOPC, BLOCK, SL, CHECK_ANY>(sv, pos, light_dir(), ts, us, vs, st, cnt);
                 if (sid >= 0) lc = 0.0f;
             }
             lbuf[depth * BLOCK] = lc;
@@ -281,7 +285,7 @@ __device__ __forceinline__ void redo_sample(const SceneView& sv, const RenderArg
     f3 o, d;
     camera_sample(a.cam, x, y, a.invW, a.invH, rng, o, d);
     TravCount cnt;
-    const f3 c = trace_path<false, BLOCK, SL, true>(sv, o, d, rng, rays_e, rays_s, st, lbuf, cnt, false);
+    const f3 c = trace_path<false, BLOCK, SL, true, false>(sv, o, d, rng, rays_e, rays_s, st, lbuf, cnt, false);
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((f32x4){c.x, c.y, c.z, 0.0f},
                                 reinterpret_cast<f32x4*>(sbuf + ((size_t)smp * sb_ss + (size_t)pix * sb_sp)));
@@ -2619,7 +2623,7 @@ static uint32_t oct_shadow_check(const Scene& s)
     const f3 ld = light_dir();
     const float l[3] = {fabsf(ld.x), fabsf(ld.y), fabsf(ld.z)};
     for (int k = 0; k < 3; ++k)
-        if (l[k] * fminf(kMinT, s.oct_grid.reach) <= 2.0f * s.oct_grid.band[k]) return 1u;
+        if (l[k] * fminf(kMinT, s.oct_grid.reach) <= s.oct_grid.drift[k]) return 1u;
     return 0u;
 }
 

@@ -287,8 +287,9 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                 // orders the indices; the tie bit never decides
                 const int id = __float_as_int(c.y);
                 // (no triangle is accepted at t == tmax, the initial bt: the
-                // flag it sets on best = -1 leaves -1)
-                const bool tie = t == ts.bt;
+                // flag it sets on best = -1 leaves -1; a triangle met again
+                // through another of its split references is no tie)
+                const bool tie = t == ts.bt && (id | 1) != (ts.best | 1);
                 if (t < ts.bt || (!FLAG && tie && id < ts.best)) {
                     ts.bt = t;
                     ts.bu = u;
@@ -351,13 +352,13 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
 #else
             // FLAG: the first triangle met keeps a tie (the flag sends the query
             // to be answered again); otherwise the lower index takes it
-            const bool tie0 = ok0 && t0 == ts.bt;
+            const bool tie0 = ok0 && t0 == ts.bt && (id0 | 1) != (ts.best | 1);  // (a split reference of best: no tie)
             const bool acc0 = ok0 && (t0 < ts.bt || (!FLAG && tie0 && id0 < ts.best));
             ts.bt = acc0 ? t0 : ts.bt;
             ts.bu = acc0 ? u0 : ts.bu;
             ts.bv = acc0 ? w0 : ts.bv;
             ts.best = (acc0 ? id0 : ts.best) | (int)tie0;
-            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt;
+            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt && (id1 | 1) != (ts.best | 1);
             const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (!FLAG && tie1 && id1 < ts.best));
             ts.bt = acc1 ? t1 : ts.bt;
             ts.bu = acc1 ? u1 : ts.bu;
@@ -517,16 +518,20 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
 // flat-triangle test evaluates it (tmpt_octree.cpp plane_dist).
 TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
 {
-    const float oc[3] = {o.x, o.y, o.z}, dc[3] = {d.x, d.y, d.z};
+    // the common case first: no axis along which the ray barely moved (one
+    // branch; the plane distances only in the rare case)
     const float span = fminf(t, g.reach);
+    const bool ax = fabsf(d.x) * span <= g.drift[0], ay = fabsf(d.y) * span <= g.drift[1],
+               az = fabsf(d.z) * span <= g.drift[2];
+    if (!(ax | ay | az)) return false;
+    const float oc[3] = {o.x, o.y, o.z}, dc[3] = {d.x, d.y, d.z};
+    const bool on[3] = {ax, ay, az};
     bool f = false;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        if (fabsf(dc[k]) * span <= 2.0f * g.band[k]) {
-            const float rel = fmaf(t, dc[k], oc[k]) - g.r0[k];
-            const float j = rintf(rel * g.inv_cell[k]);
-            f |= fabsf(fmaf(-j, g.cell[k], rel)) <= g.band[k];
-        }
+        const float rel = fmaf(t, dc[k], oc[k]) - g.r0[k];
+        const float j = rintf(rel * g.inv_cell[k]);
+        f |= on[k] && fabsf(fmaf(-j, g.cell[k], rel)) <= g.band[k];
     }
     return f;
 }
@@ -538,7 +543,11 @@ TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
 __device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& r, const TravState& ts)
 {
     if (sv.oct == nullptr || ts.best < 0) return false;
+#ifdef TMPT_EXP_NOCRACK  // cost experiment: no crack test (wrong answers on crack queries)
+    return (ts.best & 1) != 0;
+#else
     return (ts.best & 1) != 0 || octree_crack(sv.oct->grid, r.o, r.d, ts.bt);
+#endif
 }
 
 // counts a query octree_flag sent to the octree: ties[0] (bit 0) or ties[6] (crack)
@@ -598,7 +607,11 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d)
 // Whole query in one call, t in [tmin, tmax] (Scene::HitScene, scene.cpp:86-97).
 // Returns the original triangle index or -1; (bt, bu, bv) of the hit.  TOPC:
 // the caller's block holds the top BVH levels in LDS (st.top).
-template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false, bool SOA = false, bool NEG = false>
+// CHECK_ANY = false: the caller knows no shadow answer needs the octree
+// (PathCtl::oct_shadow is 0 wherever it runs), so the any-hit query skips
+// settle_any and its walk.
+template <bool ANY, bool COUNT, int BLOCK, int SL, bool TOPC = false, bool SOA = false, bool NEG = false,
+          bool CHECK_ANY = true>
 __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, float tmin,
                                         float tmax, float& bt, float& bu, float& bv,
                                         TravStack<BLOCK, SL>& st, TravCount& cnt)
@@ -610,7 +623,8 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
         while (!trav_step4q2_mixed<COUNT, BLOCK, SL, TOPC, 0, SOA, NEG>(sv, r, ANY, ts, st, cnt, tlo, tmin, tmax)) {
         }
         if (!ANY) settle_closest<BLOCK, SL, TOPC, SOA, NEG>(sv, r, tlo, tmin, tmax, ts, st);
-        else settle_any(sv, r, tmin, tmax, ts);
+        else if (CHECK_ANY) settle_any(sv, r, tmin, tmax, ts);
+        else ts.best >>= 1;
     }
     bt = ts.bt;
     bu = ts.bu;
