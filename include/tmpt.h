@@ -145,8 +145,6 @@ typedef struct {
     int32_t redo_launches;    /* sample seeding, tie_defer: k_redo launches of the last render (0 or 1) */
     double redo_ms;           /* their time; extend_ms holds the main k_path launches only */
     uint64_t redo_rays;       /* their queries (part of the render's ray count) */
-    int32_t bvh_refs;         /* references the BVH holds: n_tris, more with build option split */
-    int32_t reserved_stats;
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */
@@ -193,10 +191,6 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   leaf_max     triangles per BVH4 leaf, 1..16 (default 2)
  *   collapse     greedy (0, default) | sah (1): BVH2 -> BVH4 collapse
  *   ploc_radius  PLOC search radius, 1..256 (default 32)
- *   split        early split clipping (Ernst & Greiner 2007): a triangle whose box is
- *                larger than split/1000 of the scene's largest extent enters the BVH as
- *                pieces -- its box halved along the longest axis, each piece the box of
- *                the clipped triangle -- all pointing at the same triangle (0 = off)
  *   sah_c_leaf, sah_c_tri  SAH collapse costs (defaults 0.7, 0.5; inner node 1)
  * Render options (tmpt_scene_set_option; apply to later renders on the scene):
  *   sample_block     sample seeding: samples per work unit, power of two (0 = auto)
@@ -283,13 +277,6 @@ int tmpt_octree_digest(const float* tris, int32_t n, const float bmin[3], const 
  * {r0.xyz, 1/cell.xyz, cell.xyz, band.xyz, reach} of that octree. */
 int tmpt_octree_flags(const float* tris, int32_t n, const float bmin[3], const float bmax[3], const float* rays,
                       const float* t, const int32_t* ids, int64_t n_rays, uint8_t* flags, float grid[13]);
-/* Check hook (host only, no device): the references build option split=<split>
- * builds the BVH over (tmpt_split.cpp): returns their count; with cap >= that
- * count also ref_tri[r] (the triangle; ~index = the whole triangle) and
- * boxes[6 r ..] = a piece's box {lo, hi} (unpadded).  Tests check that the
- * pieces cover their triangles. */
-int64_t tmpt_split_references(const float* tris, int32_t n, int32_t split, int64_t cap, int32_t* ref_tri,
-                              float* boxes);
 /* Scene::~Scene (scene.h:20) */
 int tmpt_scene_destroy(tmpt_scene* scene);
 

@@ -152,12 +152,11 @@ def test_hitscene_per_ray_ranges(gpu):
 @pytest.mark.parametrize("opts", [{"builder": "lbvh"}, {"collapse": "sah"}, {"leaf_max": 4},
                                   {"builder": "lbvh", "leaf_max": 1}, {"ploc_radius": 4, "leaf_max": 16},
                                   {"collapse": "sah", "sah_c_leaf": 0.2, "sah_c_tri": 2.0}, {"layout": "soa"},
-                                  {"layout": "soa", "leaf_max": 4}, {"split": 20}, {"split": 5, "leaf_max": 4},
-                                  {"split": 30, "layout": "soa"}])
+                                  {"layout": "soa", "leaf_max": 4}])
 def test_build_variants_match_oracle(gpu, opts):
     """Every build option (LBVH builder, SAH collapse and its costs, leaf size,
-    PLOC radius, the SoA plane layout, split references) changes the tree or its layout, never the answers:
-    HitScene on 200k rays and a sample-seeded frame equal the oracle."""
+    PLOC radius, the SoA plane layout) changes the tree or its layout, never the answers: HitScene on 200k
+    rays and a sample-seeded frame equal the oracle."""
     tris, bmin, bmax = tm.load_scene(data("teapot.obj"))
     sc = tm.Scene(tris, options=opts)
     rays = _random_rays(tris, 200_000, seed=13)
@@ -1219,31 +1218,3 @@ def test_hitscene_negative_single_range(gpu):
         h = ids >= 0
         assert np.array_equal(hits[h].view(np.uint32), ohits[h].view(np.uint32))
     sc.close()
-
-
-@pytest.mark.parametrize("split", [10, 30])
-def test_split_references_reference_answers(gpu, sponza_path, split):
-    """Build option split on the bench scene, with the reference's octree: the
-    pieces of a large triangle all point at it, so a ray meeting it through
-    two pieces is no tie (tmpt_traverse.h) -- the adversarial KAT's answers and
-    a sample-seeded frame (64 spp, every 64th row, deferred ties) equal the
-    oracle octree's; the tie count equals the unsplit scene's."""
-    import octree_kat as K
-    tris, bmin, bmax = tm.load_scene(sponza_path)
-    w, h, spp = 480, 270, 16
-    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
-    osc = _ref_oracle(tris, bmin, bmax)
-    rays = _random_rays(tris, 60_000, seed=17)
-    with tm.Scene(tris, bounds=(bmin, bmax)) as base:
-        bimg, brays = base.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
-        bties = base.stats().tie_queries
-    with tm.Scene(tris, bounds=(bmin, bmax), options={"split": split}) as sc:
-        assert sc.stats().bvh_refs > len(tris)
-        ids, hits = sc.hit_scene_batch(rays, 0.001, 1.0e7)
-        img, nrays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, band_rows=1)
-        st = sc.stats()
-    _same_answers(ids, hits, *osc.hit_batch(rays, 0.001, 1.0e7))
-    assert nrays == brays and np.array_equal(img, bimg) and st.tie_queries == bties
-    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE, row_step=16)
-    rows = np.arange(0, h, 16)
-    assert np.array_equal(img[rows], ref[rows])

@@ -94,38 +94,3 @@ def test_crack_wall_is_flat_and_lost():
     # the scene's own triangles are not flat (teapot has no triangle on a plane)
     f_all, _ = tm.octree_flags(tris, lo, hi, rays[:1], np.ones(1, np.float32), np.zeros(1, np.int32))
     assert f_all[0] & 1 == 0
-
-
-@pytest.mark.parametrize("name,split", [("teapot", 20), ("cube", 100), ("grid", 30)])
-def test_split_references_cover_their_triangles(name, split):
-    """Build option split (tmpt_split.cpp): every piece belongs to a split
-    triangle, and points all over each split triangle -- its vertices, edge
-    points and interior points -- lie in at least one of its pieces' boxes
-    (so culling by the pieces stays conservative)."""
-    import os
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "data"))
-    import gen_standin_sponza
-    tris, bmin, bmax = _scene(name)
-    if name == "teapot":  # and the bench scene's large walls and slabs
-        tris = np.concatenate([tris, oracle.load_scene(gen_standin_sponza.ensure())[0][-3000:]])
-    ref, boxes = tm.split_references(tris, split)
-    whole = ref < 0
-    assert len(ref) >= len(tris) and np.array_equal(np.unique(np.where(whole, ~ref, ref)), np.arange(len(tris)))
-    pieces = ~whole
-    split_ids = np.unique(ref[pieces])
-    assert (np.intersect1d(split_ids, ~ref[whole]).size == 0)  # a triangle is whole or in pieces
-    rng = np.random.default_rng(0)
-    for t in split_ids[:400]:
-        b = boxes[ref == t].astype(np.float64)
-        bary = rng.random((256, 3)) ** 3
-        bary[:3] = np.eye(3)
-        bary[np.arange(3, 30), rng.integers(0, 3, 27)] = 0.0  # edge points
-        bary /= bary.sum(1, keepdims=True)
-        pts = bary @ tris[t].astype(np.float64)
-        # (the interpolated points carry float64 rounding off the plane: a
-        # tolerance far inside the device's own padding, kBoxPadRel = 1e-5)
-        tol = 1e-9 * (np.abs(pts) + 1.0)
-        inside = ((pts[:, None, :] >= b[None, :, :3] - tol[:, None, :]) &
-                  (pts[:, None, :] <= b[None, :, 3:] + tol[:, None, :])).all(2).any(1)
-        assert inside.all(), (t, pts[~inside][:3])

@@ -30,7 +30,7 @@ import numpy as np
 __all__ = [
     "Camera", "Scene", "Hit", "RenderStats", "load_scene", "write_png", "device_count",
     "SEED_ROW", "SEED_PIXEL", "SEED_SAMPLE", "ENGINE_WAVEFRONT", "ENGINE_MEGAKERNEL", "ENGINE_PERSISTENT", "lib_path", "TmptError",
-    "tile_rows", "tile_row_to_y", "render_multi", "octree_bounds", "octree_digest", "octree_flags", "split_references",
+    "tile_rows", "tile_row_to_y", "render_multi", "octree_bounds", "octree_digest", "octree_flags",
 ]
 
 SEED_ROW, SEED_PIXEL, SEED_SAMPLE = 0, 1, 2
@@ -109,7 +109,7 @@ class _Stats(ctypes.Structure):
                 ("redo_samples", ctypes.c_int64), ("redo_late", ctypes.c_int64),
                 ("crack_queries", ctypes.c_uint64), ("octree_flat", ctypes.c_int32),
                 ("redo_launches", ctypes.c_int32), ("redo_ms", ctypes.c_double),
-                ("redo_rays", ctypes.c_uint64), ("bvh_refs", ctypes.c_int32), ("reserved_stats", ctypes.c_int32)]
+                ("redo_rays", ctypes.c_uint64)]
 
 
 def _sig(name, res, args):
@@ -145,8 +145,6 @@ _render = _sig("tmpt_render", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(_Ca
 _build_octree = _sig("tmpt_scene_build_octree", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p])
 _octree_bounds = _sig("tmpt_octree_bounds", ctypes.c_int, [_f32p, _f32p, _f32p])
 _octree_digest = _sig("tmpt_octree_digest", ctypes.c_int, [_f32p, ctypes.c_int32, _f32p, _f32p, _u64p])
-_split_refs = _sig("tmpt_split_references", ctypes.c_int64, [_f32p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
-                                                            _i32p, _f32p])
 _octree_flags = _sig("tmpt_octree_flags", ctypes.c_int, [_f32p, ctypes.c_int32, _f32p, _f32p, _f32p, _f32p, _i32p,
                                                          ctypes.c_int64, ctypes.c_void_p, _f32p])
 _render_multi = _sig("tmpt_render_multi", ctypes.c_int,
@@ -169,7 +167,7 @@ EXPORTS = ("tmpt_load_obj", "tmpt_free", "tmpt_camera_init", "tmpt_camera_for_sc
            "tmpt_render", "tmpt_render_multi", "tmpt_tile_rows", "tmpt_tile_row_to_y", "tmpt_get_stats",
            "tmpt_write_png", "tmpt_last_error", "tmpt_abi_version", "tmpt_unit_sincos",
            "tmpt_scene_build_octree", "tmpt_octree_bounds", "tmpt_octree_digest",
-           "tmpt_octree_flags", "tmpt_split_references")
+           "tmpt_octree_flags")
 
 
 def _check(rc: int, what: str) -> None:
@@ -250,20 +248,6 @@ def octree_flags(tris: np.ndarray, box_min, box_max, rays, t, ids):
     _check(_octree_flags(_fp(tr), tr.shape[0], _fp(lo), _fp(hi), _fp(r), _fp(tt), ii.ctypes.data_as(_i32p),
                          r.shape[0], out.ctypes.data, _fp(grid)), "octree_flags")
     return out, grid
-
-
-def split_references(tris: np.ndarray, split: int):
-    """The references build option split=<split> builds the BVH over (host, no
-    GPU): (ref_tri: the triangle of each, ~index for a whole triangle; boxes
-    n x 6 of the pieces, unpadded)."""
-    tr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
-    n = int(_split_refs(_fp(tr), tr.shape[0], split, 0, None, None))
-    if n < 0:
-        raise TmptError(f"split_references failed ({n}): {_last_error().decode(errors='replace')}")
-    ref = np.zeros(n, np.int32)
-    boxes = np.zeros((n, 6), np.float32)
-    _split_refs(_fp(tr), tr.shape[0], split, n, ref.ctypes.data_as(_i32p), _fp(boxes))
-    return ref, boxes
 
 
 # ----------------------------------------------------------------------------- camera
@@ -366,8 +350,6 @@ class RenderStats:
     redo_launches: int
     redo_ms: float
     redo_rays: int
-    bvh_refs: int
-    reserved_stats: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

@@ -109,7 +109,6 @@ const OptionDef kOptions[] = {
     {"leaf_max", true, 1, kLeafMaxTris, &Options::leaf_max, nullptr, nullptr},
     {"collapse", true, 0, 1, &Options::collapse, nullptr, nullptr},
     {"ploc_radius", true, 1, 256, &Options::ploc_radius, nullptr, nullptr},
-    {"split", true, 0, 1000, &Options::split, nullptr, nullptr},
     {"sah_c_leaf", true, 0, 1e6, nullptr, &Options::sah_c_leaf, nullptr},
     {"sah_c_tri", true, 0, 1e6, nullptr, &Options::sah_c_tri, nullptr},
     {"sample_block", false, 0, 1024, &Options::sample_block, nullptr, nullptr},
@@ -560,22 +559,6 @@ int tmpt_octree_flags(const float* tris, int32_t n, const float bmin[3], const f
     TMPT_GUARD_END
 }
 
-int64_t tmpt_split_references(const float* tris, int32_t n, int32_t split, int64_t cap, int32_t* ref_tri,
-                              float* boxes)
-{
-    TMPT_GUARD_BEGIN
-    if (n < 0 || (n > 0 && !tris) || split < 1 || split > 1000) return bad("tmpt_split_references: bad arguments");
-    std::vector<float> b;
-    std::vector<int32_t> r;
-    const int32_t nr = split_references(tris, n, (float)split * 1e-3f, b, r);
-    if (cap >= nr && ref_tri && boxes) {
-        std::copy(r.begin(), r.end(), ref_tri);
-        std::copy(b.begin(), b.end(), boxes);
-    }
-    return nr;
-    TMPT_GUARD_END
-}
-
 int tmpt_scene_set_option(tmpt_scene* h, const char* key, double value)
 {
     TMPT_GUARD_BEGIN
@@ -919,8 +902,6 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->redo_launches = s.redo_launches;
     o->redo_ms = s.redo_ms;
     o->redo_rays = s.redo_rays;
-    o->bvh_refs = s.n_refs;
-    o->reserved_stats = 0;
     return 0;
 }
 

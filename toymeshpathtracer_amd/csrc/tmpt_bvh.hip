@@ -102,59 +102,6 @@ __global__ void __launch_bounds__(kBlock) k_tri_prep(const float* __restrict__ t
     }
 }
 
-// Split references (build option split, tmpt_split.cpp): reference r is the
-// whole triangle ~ref_tri[r] (its padded box and centroid as k_tri_prep made
-// them) or a piece of triangle ref_tri[r] with box rbox[6 r ..], padded as
-// k_tri_prep pads a triangle's box.  Centroid bounds as k_tri_prep's.
-__global__ void __launch_bounds__(kBlock) k_ref_prep(const int32_t* __restrict__ ref_tri,
-                                                     const float* __restrict__ rbox, int32_t nr, int32_t n,
-                                                     Soa6 tbox, const float* __restrict__ tcent, Soa6 box,
-                                                     float* __restrict__ cent, uint32_t* __restrict__ cbounds)
-{
-    __shared__ uint32_t red[6][kBlock / 64];
-    int i = blockIdx.x * kBlock + threadIdx.x;
-    float c[3] = {INFINITY, INFINITY, INFINITY};
-    float cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
-    if (i < nr) {
-        const int32_t t = ref_tri[i];
-        float cx, cy, cz;
-        if (t < 0) {
-            const int32_t w = ~t;
-            box.lx[i] = tbox.lx[w]; box.ly[i] = tbox.ly[w]; box.lz[i] = tbox.lz[w];
-            box.hx[i] = tbox.hx[w]; box.hy[i] = tbox.hy[w]; box.hz[i] = tbox.hz[w];
-            cx = tcent[w]; cy = tcent[n + w]; cz = tcent[2 * n + w];
-        } else {
-            const float* b = rbox + 6 * (int64_t)i;
-            const f3 lo = mk(b[0], b[1], b[2]), hi = mk(b[3], b[4], b[5]);
-            float px = kBoxPadRel * (fmaxf(fabsf(lo.x), fabsf(hi.x)) + (hi.x - lo.x)) + 1e-30f;
-            float py = kBoxPadRel * (fmaxf(fabsf(lo.y), fabsf(hi.y)) + (hi.y - lo.y)) + 1e-30f;
-            float pz = kBoxPadRel * (fmaxf(fabsf(lo.z), fabsf(hi.z)) + (hi.z - lo.z)) + 1e-30f;
-            box.lx[i] = lo.x - px; box.ly[i] = lo.y - py; box.lz[i] = lo.z - pz;
-            box.hx[i] = hi.x + px; box.hy[i] = hi.y + py; box.hz[i] = hi.z + pz;
-            cx = 0.5f * (lo.x + hi.x); cy = 0.5f * (lo.y + hi.y); cz = 0.5f * (lo.z + hi.z);
-        }
-        cent[i] = cx; cent[nr + i] = cy; cent[2 * nr + i] = cz;
-        c[0] = cmax[0] = cx; c[1] = cmax[1] = cy; c[2] = cmax[2] = cz;
-    }
-    uint32_t v[6] = {f2ord(c[0]), f2ord(c[1]), f2ord(c[2]),
-                     f2ord(cmax[0]), f2ord(cmax[1]), f2ord(cmax[2])};
-    for (int off = 32; off > 0; off >>= 1) {
-        for (int k = 0; k < 3; ++k) v[k] = min(v[k], (uint32_t)__shfl_xor((int)v[k], off));
-        for (int k = 3; k < 6; ++k) v[k] = max(v[k], (uint32_t)__shfl_xor((int)v[k], off));
-    }
-    int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0)
-        for (int k = 0; k < 6; ++k) red[k][wave] = v[k];
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        int k = threadIdx.x;
-        uint32_t r = red[k][0];
-        for (int w = 1; w < kBlock / 64; ++w) r = k < 3 ? min(r, red[k][w]) : max(r, red[k][w]);
-        if (k < 3) atomicMin(&cbounds[k], r);
-        else atomicMax(&cbounds[k], r);
-    }
-}
-
 __device__ __forceinline__ uint32_t expand10(uint32_t v)
 {
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -710,16 +657,11 @@ __global__ void __launch_bounds__(kBlock) k_bvh4_level(const int2* __restrict__ 
 
 __global__ void __launch_bounds__(kBlock) k_tri_pre(const float* __restrict__ tris9, int32_t n,
                                                     const uint32_t* __restrict__ vals,
-                                                    TriPre* __restrict__ pre,
-                                                    const int32_t* __restrict__ ref_tri = nullptr)
+                                                    TriPre* __restrict__ pre)
 {
     int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= n) return;
     int o = (int)vals[k];
-    if (ref_tri) {  // split references: the triangle of reference o
-        const int32_t t = ref_tri[o];
-        o = t < 0 ? ~t : t;
-    }
     const float* t = tris9 + 9 * (int64_t)o;
     f3 v0 = mk(t[0], t[1], t[2]), v1 = mk(t[3], t[4], t[5]), v2 = mk(t[6], t[7], t[8]);
     f3 e1 = v1 - v0, e2 = v2 - v0;  // maths.cpp:341-342, same roundings
@@ -782,8 +724,7 @@ int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat)
             return -1;
         }
     }
-    k_mark_flat<<<blocks_for(s.n_refs, kBlock), kBlock, 0, s.stream>>>(s.tri_pre, const_cast<float2*>(s.soa.tc),
-                                                                        s.n_refs, d);
+    k_mark_flat<<<blocks_for(s.n, kBlock), kBlock, 0, s.stream>>>(s.tri_pre, const_cast<float2*>(s.soa.tc), s.n, d);
     const hipError_t e = hipGetLastError();
     const hipError_t e2 = hipStreamSynchronize(s.stream);
     if (d) (void)hipFree(d);
@@ -794,7 +735,7 @@ int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat)
 
 int build_soa(Scene& s)
 {
-    const size_t n4 = (size_t)std::max(s.n_nodes4, 1), n1 = (size_t)s.n_refs + 1;
+    const size_t n4 = (size_t)std::max(s.n_nodes4, 1), n1 = (size_t)s.n + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t o_nb = al(16 * n4), o_nc = o_nb + al(16 * n4), o_nd = o_nc + al(8 * n4), o_ta = o_nd + al(16 * n4),
                  o_tb = o_ta + al(16 * n1), o_tc = o_tb + al(16 * n1), total = o_tc + al(8 * n1);
@@ -842,17 +783,9 @@ size_t radix_sort_hist_words(int32_t n) { return 256 * (size_t)std::max(1, block
 
 int build_lbvh(Scene& s, const float* d_tris9)
 {
-    const int32_t ntri = s.n;
+    const int32_t n = s.n;
     hipStream_t st = s.stream;
     auto t0 = std::chrono::steady_clock::now();
-    // build option split: the BVH is built over references (pieces of the
-    // large triangles, tmpt_split.cpp); n counts the primitives from here on
-    std::vector<float> rbox;
-    std::vector<int32_t> rtri;
-    const int32_t n = s.opt.split > 0 && ntri > 0
-                          ? split_references(s.tris_host.data(), ntri, (float)s.opt.split * 1e-3f, rbox, rtri)
-                          : ntri;
-    s.n_refs = n;
     const int32_t m = n >= 2 ? n - 1 : 1;  // internal nodes
     s.n_nodes = m;
     TMPT_HIP(hipMalloc(&s.nodes4, sizeof(Bvh4Node) * (size_t)m));
@@ -860,7 +793,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
     // empty BVH4 child slots link to
     TMPT_HIP(hipMalloc(&s.tri_pre, sizeof(TriPre) * ((size_t)n + 1)));
     TMPT_HIP(hipMemsetAsync(s.tri_pre + n, 0, sizeof(TriPre), st));
-    TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(ntri, 1)));
+    TMPT_HIP(hipMalloc(&s.tri_orig, sizeof(TriOrig) * (size_t)std::max(n, 1)));
     if (n == 0) {
         TMPT_HIP(hipMemsetAsync(s.nodes4, 0, sizeof(Bvh4Node), st));
         s.max_depth = 0;
@@ -883,17 +816,6 @@ int build_lbvh(Scene& s, const float* d_tris9)
     float* leafbuf = (float*)alloc(6 * nn * sizeof(float));
     float* ibbuf = (float*)alloc(6 * (size_t)m * sizeof(float));
     float* cent = (float*)alloc(3 * nn * sizeof(float));
-    const bool split = !rtri.empty();
-    // split: the triangles' own boxes and centroids first, then the references'
-    float* tleafbuf = split ? (float*)alloc(6 * (size_t)ntri * sizeof(float)) : leafbuf;
-    float* tcent = split ? (float*)alloc(3 * (size_t)ntri * sizeof(float)) : cent;
-    int32_t* d_rtri = split ? (int32_t*)alloc(nn * 4) : nullptr;
-    float* d_rbox = split ? (float*)alloc(6 * nn * sizeof(float)) : nullptr;
-    if (split && (!tleafbuf || !tcent || !d_rtri || !d_rbox)) {
-        free_all();
-        set_error("build_lbvh: out of device memory (split references)");
-        return -1;
-    }
     uint32_t* cb = (uint32_t*)alloc(6 * sizeof(uint32_t));
     uint32_t* k0 = (uint32_t*)alloc(nn * 4);
     uint32_t* v0 = (uint32_t*)alloc(nn * 4);
@@ -924,20 +846,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
     do {
         if (hipMemcpyAsync(cb, init, sizeof(init), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
         if (hipMemsetAsync(maxd, 0, 4, st) != hipSuccess) { rc = -1; break; }
-        if (split) {
-            const size_t t6 = (size_t)ntri;
-            Soa6 tleaf{tleafbuf, tleafbuf + t6, tleafbuf + 2 * t6, tleafbuf + 3 * t6, tleafbuf + 4 * t6,
-                       tleafbuf + 5 * t6};
-            k_tri_prep<<<blocks_for(ntri, kBlock), kBlock, 0, st>>>(d_tris9, ntri, s.tri_orig, tleaf, tcent, cb);
-            if (hipMemcpyAsync(d_rtri, rtri.data(), nn * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(d_rbox, rbox.data(), 6 * nn * sizeof(float), hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(cb, init, sizeof(init), hipMemcpyHostToDevice, st) != hipSuccess) { rc = -1; break; }
-            k_ref_prep<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_rtri, d_rbox, n, ntri, tleaf, tcent, leaf, cent, cb);
-            // the host vectors must outlive the copies
-            if (hipStreamSynchronize(st) != hipSuccess) { rc = -1; break; }
-        } else {
-            k_tri_prep<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, s.tri_orig, leaf, cent, cb);
-        }
+        k_tri_prep<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, s.tri_orig, leaf, cent, cb);
         k_morton<<<blocks_for(n, kBlock), kBlock, 0, st>>>(cent, n, cb, k0, v0);
         uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
         for (int pass = 0; pass < 4; ++pass) {
@@ -1034,7 +943,7 @@ int build_lbvh(Scene& s, const float* d_tris9)
             troot = m - 1;  // the last merge creates the root
             s.ploc_iters = it;
         }
-        k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, tvals, s.tri_pre, d_rtri);
+        k_tri_pre<<<blocks_for(n, kBlock), kBlock, 0, st>>>(d_tris9, n, tvals, s.tri_pre);
         // binary tree -> BVH4Q, top-down, one launch per level
         const int leaf_max = s.opt.leaf_max;
         s.leaf_max = leaf_max;

@@ -170,7 +170,6 @@ struct Options {
     int leaf_max = 2;     // triangles per BVH4 leaf, 1..kLeafMaxTris
     int collapse = 0;     // BVH2 -> BVH4: 0 = greedy largest-area opening, 1 = SAH-optimal
     int ploc_radius = 32; // PLOC nearest-neighbour search radius
-    int split = 0;        // early split clipping: triangles larger than split/1000 of the scene (0 = off)
     float sah_c_leaf = 0.7f, sah_c_tri = 0.5f;  // SAH collapse costs (inner node = 1)
     // render (tmpt_scene_set_option)
     int sample_block = 0;     // sample seeding: samples per work unit, a power of two (0 = auto)
@@ -211,7 +210,6 @@ int options_get(const Options& o, const char* key, double* value);
 struct Scene {
     int device = 0;
     int32_t n = 0;          // triangles incl. the floor
-    int32_t n_refs = 0;     // references the BVH is built over (= n without split; TriPre records)
     int32_t n_nodes = 0;    // internal nodes of the binary tree the BVH4 is collapsed from
     int32_t max_depth = 0;  // of the LBVH (Karras builder)
     Bvh4Node* nodes4 = nullptr;
@@ -315,12 +313,6 @@ const char* last_error();
 // tmpt_bvh.hip
 int build_lbvh(Scene& s, const float* d_tris9);
 int build_soa(Scene& s);  // layout=soa planes from the built AoS records
-// tmpt_split.cpp: early split clipping (build option split): the references
-// the BVH is built over -- ref_tri[r] = the triangle (~index: the whole
-// triangle), boxes[6 r ..] = a piece's box {lo, hi} -- for triangles whose box
-// is larger than frac x the scene's largest extent; returns their count
-int32_t split_references(const float* tris9, int32_t n, float frac, std::vector<float>& boxes,
-                         std::vector<int32_t>& ref_tri);
 // the octree's flat triangles marked in the leaf-ordered records (bit 0 of the
 // doubled index), the others cleared; flat has s.n entries (empty: clear all)
 int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat);

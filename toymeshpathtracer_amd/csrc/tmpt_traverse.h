@@ -287,9 +287,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                 // orders the indices; the tie bit never decides
                 const int id = __float_as_int(c.y);
                 // (no triangle is accepted at t == tmax, the initial bt: the
-                // flag it sets on best = -1 leaves -1; a triangle met again
-                // through another of its split references is no tie)
-                const bool tie = t == ts.bt && (id | 1) != (ts.best | 1);
+                // flag it sets on best = -1 leaves -1)
+                const bool tie = t == ts.bt;
                 if (t < ts.bt || (!FLAG && tie && id < ts.best)) {
                     ts.bt = t;
                     ts.bu = u;
@@ -352,13 +351,13 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
 #else
             // FLAG: the first triangle met keeps a tie (the flag sends the query
             // to be answered again); otherwise the lower index takes it
-            const bool tie0 = ok0 && t0 == ts.bt && (id0 | 1) != (ts.best | 1);  // (a split reference of best: no tie)
+            const bool tie0 = ok0 && t0 == ts.bt;
             const bool acc0 = ok0 && (t0 < ts.bt || (!FLAG && tie0 && id0 < ts.best));
             ts.bt = acc0 ? t0 : ts.bt;
             ts.bu = acc0 ? u0 : ts.bu;
             ts.bv = acc0 ? w0 : ts.bv;
             ts.best = (acc0 ? id0 : ts.best) | (int)tie0;
-            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt && (id1 | 1) != (ts.best | 1);
+            const bool tie1 = ok1 && !(any && acc0) && t1 == ts.bt;
             const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (!FLAG && tie1 && id1 < ts.best));
             ts.bt = acc1 ? t1 : ts.bt;
             ts.bu = acc1 ? u1 : ts.bu;
