@@ -2314,6 +2314,8 @@ SceneView view(const Scene& s)
     v.soa = s.soa;
     if (s.oct && s.opt.tie_rule == 0) {  // the reference's visit order for ties
         v.oct = s.oct_view;
+        const OctGrid& g = s.oct_grid;
+        v.crack = make_float4(g.reach, g.drift[0], g.drift[1], g.drift[2]);
     }
     return v;
 }

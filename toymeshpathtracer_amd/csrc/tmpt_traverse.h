@@ -138,6 +138,10 @@ struct SceneView {
     // one pointer to its device-side view, read only by the rare flagged
     // queries (the kernels keep one SGPR pair live for it, not four)
     const OctView* __restrict__ oct = nullptr;
+    // the crack test's first stage (octree_flag), by value so every finished
+    // query reads it from kernel-argument registers, not through `oct`:
+    // {reach, drift.xyz} of OctGrid
+    float4 crack = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     // build option layout=soa (tmpt_internal.h SoaScene): the same nodes and
     // triangle records as planes, read by the SOA instantiations
     SoaScene soa;
@@ -515,14 +519,10 @@ __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, f
 // gap between two subtrees' boxes can hide the leaves that hold the triangle
 // from the reference's walk.  The plane distance is evaluated as the host's
 // flat-triangle test evaluates it (tmpt_octree.cpp plane_dist).
-TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
+// The second stage: for the axes whose drift the first stage flagged, whether
+// the hit point lies within band of a plane of that axis.
+TMPT_HD bool octree_crack_planes(const OctGrid& g, f3 o, f3 d, float t, bool ax, bool ay, bool az)
 {
-    // the common case first: no axis along which the ray barely moved (one
-    // branch; the plane distances only in the rare case)
-    const float span = fminf(t, g.reach);
-    const bool ax = fabsf(d.x) * span <= g.drift[0], ay = fabsf(d.y) * span <= g.drift[1],
-               az = fabsf(d.z) * span <= g.drift[2];
-    if (!(ax | ay | az)) return false;
     const float oc[3] = {o.x, o.y, o.z}, dc[3] = {d.x, d.y, d.z};
     const bool on[3] = {ax, ay, az};
     bool f = false;
@@ -535,6 +535,15 @@ TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
     return f;
 }
 
+// Both stages (the host check hook's form of the device test).
+TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
+{
+    const float span = fminf(t, g.reach);
+    const bool ax = fabsf(d.x) * span <= g.drift[0], ay = fabsf(d.y) * span <= g.drift[1],
+               az = fabsf(d.z) * span <= g.drift[2];
+    return (ax | ay | az) && octree_crack_planes(g, o, d, t, ax, ay, az);
+}
+
 // Whether a finished query is one the octree answers: bit 0 of TravState::best
 // (a tie on t, or a triangle lying flat on an octree plane -- its record's
 // index is odd) or a hit that may lie in a crack.  The any-hit query's bit 0
@@ -542,10 +551,16 @@ TMPT_HD bool octree_crack(const OctGrid& g, f3 o, f3 d, float t)
 __device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& r, const TravState& ts)
 {
     if (sv.oct == nullptr || ts.best < 0) return false;
+    if ((ts.best & 1) != 0) return true;
 #ifdef TMPT_EXP_NOCRACK  // cost experiment: no crack test (wrong answers on crack queries)
-    return (ts.best & 1) != 0;
+    return false;
 #else
-    return (ts.best & 1) != 0 || octree_crack(sv.oct->grid, r.o, r.d, ts.bt);
+    // first stage from the by-value copy (no memory round trip); the plane
+    // distances, rarely needed, through the view
+    const float span = fminf(ts.bt, sv.crack.x);
+    const bool ax = fabsf(r.d.x) * span <= sv.crack.y, ay = fabsf(r.d.y) * span <= sv.crack.z,
+               az = fabsf(r.d.z) * span <= sv.crack.w;
+    return (ax | ay | az) && octree_crack_planes(sv.oct->grid, r.o, r.d, ts.bt, ax, ay, az);
 #endif
 }
 
