@@ -84,21 +84,43 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def visible_gpus_without_hip() -> int:
+    """GPUs this process would see, counted without touching HIP: the KFD
+    topology's GPU nodes (simd_count > 0), narrowed by the visibility
+    variables.  0 without a KFD (no GPU HIP could open); -1 when the topology
+    is there but unreadable (each rank then checks its own LOCAL_RANK)."""
+    nodes = "/sys/class/kfd/kfd/topology/nodes"
+    if not os.path.isdir(nodes):
+        return 0
+    try:
+        n = 0
+        for d in os.listdir(nodes):
+            with open(os.path.join(nodes, d, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            n += int(props.get("simd_count", "0")) > 0
+    except (OSError, ValueError):
+        return -1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks_if_needed() -> None:
     """--gpus N without a launcher: run N ranks under torch.distributed.run (a
-    child process; this one has made no GPU call -- counting devices does not
-    initialise them -- and exits with the child's code).  Fails loudly when
-    nccl would need more GPUs than are visible."""
+    child process; this one makes no HIP call -- it counts GPUs from the KFD
+    topology -- and exits with the child's code).  Fails loudly when nccl
+    would need more GPUs than are visible."""
     args = parse_args()
     if "WORLD_SIZE" in os.environ or args.gpus <= 1:
         return
-    import torch
-    ndev = torch.cuda.device_count()
-    if args.dist_backend == "nccl" and ndev < args.gpus:
+    ndev = visible_gpus_without_hip()
+    if args.dist_backend == "nccl" and 0 <= ndev < args.gpus:
         print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL (one rank per GPU); "
               f"{ndev} visible", file=sys.stderr, flush=True)
         sys.exit(2)
-    if ndev < 1:
+    if ndev == 0:
         print("bench.py: no GPU visible", file=sys.stderr, flush=True)
         sys.exit(2)
     with socket.socket() as sk:
@@ -330,6 +352,9 @@ def main() -> None:
         sys.exit(2)
     dist_on = world > 1 or args.force_dist  # the collective path (process group, gather, reductions)
     ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= ndev:
+        log(f"bench.py: rank {rank} has LOCAL_RANK {local} but {ndev} visible GPUs (RCCL needs one GPU per rank)")
+        sys.exit(2)
     local = local % max(ndev, 1) if args.dist_backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")

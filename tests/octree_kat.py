@@ -312,3 +312,30 @@ def crack_wall_rays(wall, ax, n, seed):
     off[:, w] = rng.normal(size=n) * 0.5
     o = pts + off
     return np.concatenate([o, _unit(pts - o)], 1).astype(np.float32)
+
+
+def child_order_case():
+    """A tie whose reference answer follows from scene.cpp's structure alone,
+    derived by hand (the visit order pinned independently of the
+    oracle).  Root box [-1, 1]^3, 12 triangles, so the root splits
+    (scene.cpp:101; 17 nodes: child 6 holds Tb and the fillers and splits
+    again); children are built min-corner first (:119-141) and
+    visited in that order (:44-49), child 0 = [-1, 0]^3, child 7 = [0, 1]^3.
+      Ta (index 0): small, around p = (0.5, 0.5, 0.5), inside child 7 only;
+      Tb (index 1): large, coplanar with Ta (plane z = x), through p, with a
+                    vertex at (-0.75, -0.75, -0.75) inside child 0;
+      10 fillers near (-0.9, 0.9, 0.9), off the ray.
+    The ray o = (-0.75, -0.75, -0.25), d = (1.25, 1.25, 0.75) starts in child 0
+    and hits both at exactly t = 1 (dyadic coordinates: every Moller-Trumbore
+    step is exact).  The walk meets Tb in child 0 first; Ta, met in child 7 at
+    the same t, is not nearer (strict '<', scene.cpp:34).  So the reference
+    answers Tb, index 1; the lowest-index rule answers Ta."""
+    ta = [[0.25, 0.25, 0.25], [0.75, 0.25, 0.75], [0.5, 0.75, 0.5]]
+    tb = [[-0.75, -0.75, -0.75], [0.75, -0.75, 0.75], [0.75, 0.875, 0.75]]
+    fill = [[[-0.9 + 0.01 * i, 0.9, 0.9], [-0.9 + 0.01 * i, 0.92, 0.9], [-0.9 + 0.01 * i, 0.9, 0.92]]
+            for i in range(10)]
+    tris = np.array([ta, tb] + fill, np.float32)
+    ray = np.array([[-0.75, -0.75, -0.25, 1.25, 1.25, 0.75]], np.float32)
+    box = (np.full(3, -1.0, np.float32), np.full(3, 1.0, np.float32))
+    return tris, ray, box
+

@@ -114,6 +114,24 @@ def test_hitscene_kat(gpu, name):
     sc.close()
 
 
+def test_hitscene_child_order_tie(gpu):
+    """The hand-derived visit-order tie (tests/octree_kat.py child_order_case):
+    two coplanar triangles at exactly t = 1, met in octree children 0 and 7.
+    The reference's walk answers index 1 (child 0 first, scene.cpp:44-49); the
+    lowest-index rule answers 0.  Pins the tie order without the oracle."""
+    import octree_kat as K
+    tris, ray, (lo, hi) = K.child_order_case()
+    sc = tm.Scene(tris)
+    sc.build_octree(lo, hi)
+    assert sc.stats().octree_nodes == 17
+    ids, hits = sc.hit_scene_batch(ray, 0.001, 1.0e7)
+    assert ids[0] == 1 and hits[0, 6] == 1.0 and sc.stats().tie_queries >= 1
+    sc.set_option("tie_rule", 1)
+    ids, hits = sc.hit_scene_batch(ray, 0.001, 1.0e7)
+    assert ids[0] == 0 and hits[0, 6] == 1.0
+    sc.close()
+
+
 def test_hitscene_per_ray_ranges(gpu):
     """tmpt_scene_hit_ranged: HitScene(ray, tMin, tMax, hit) with the range per
     ray, as scene.h:36-37 takes it (SURVEY §8b rays8 = {o, d, tmin, tmax}).

@@ -94,3 +94,21 @@ def test_crack_wall_is_flat_and_lost():
     # the scene's own triangles are not flat (teapot has no triangle on a plane)
     f_all, _ = tm.octree_flags(tris, lo, hi, rays[:1], np.ones(1, np.float32), np.zeros(1, np.int32))
     assert f_all[0] & 1 == 0
+
+
+def test_child_order_case_pins_the_oracle():
+    """The oracle's octree gives the hand-derived answer (Tb, t = 1) and its
+    exact-semantics BVH the lowest index (Ta)."""
+    tris, ray, _ = K.child_order_case()
+    # oracle.Scene takes OBJ bounds and pads them by 0.7 x size (main.cpp:296-297): pass
+    # bounds whose padded box is [-1, 1]^3 exactly
+    s = np.float32(1.0 / 2.4)
+    ob = (np.full(3, -s, np.float32), np.full(3, s, np.float32))
+    octree = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=ob[0], bmax=ob[1])
+    boxes, info = octree.octree_nodes()
+    assert np.allclose(boxes[0], [-1, -1, -1, 1, 1, 1]) and len(boxes) == 17 and info[0, 0] == 1
+    ids, hits = octree.hit_batch(ray, 0.001, 1.0e7)
+    assert ids[0] == 1 and hits[0, 6] == 1.0
+    ex = oracle.Scene(tris, accel=oracle.ACCEL_LINEAR)
+    eids, ehits = ex.hit_batch(ray, 0.001, 1.0e7)
+    assert eids[0] == 0 and ehits[0, 6] == 1.0
