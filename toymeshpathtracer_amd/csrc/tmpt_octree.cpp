@@ -4,9 +4,13 @@
 // hit over all triangles.  The reference walks an 8-way octree instead
 // (scene.cpp:21-52) and keeps the FIRST triangle of the smallest t in its
 // depth-first visit order, and its root box test can drop a ray that only
-// grazes the root.  The traversal flags the queries where that can matter (a
-// tie on t); those, and only those, are answered again over this octree on
-// the device (tmpt_traverse.h octree_closest).  So the octree has to be the
+// grazes the root.  The traversal flags the queries where that can matter --
+// a tie on t; a closest hit near one of the octree's finest-level planes on a
+// ray that runs almost within that plane, where the 1-2 ulp cracks between
+// sibling boxes (min + half + half) can hide the hit (octree_grid); a hit on
+// a triangle flat in such a plane, which may be in no leaf at all
+// (octree_flat_triangles) -- and those, and only those, are answered again
+// over this octree on the device (tmpt_traverse.h octree_closest, octree_flag).  So the octree has to be the
 // reference's node for node: the same boxes (bmin/bmax halved in float,
 // scene.cpp:109-141), the same triangle lists (the separating-axis overlap
 // test of maths.cpp:165-298 in its own rounding order), the same limits

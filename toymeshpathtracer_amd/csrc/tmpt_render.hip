@@ -1764,14 +1764,21 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     if (DEFER && pc.redo_inline) {
         // Redo phase: the wave's main loop is over; it traces the samples the
         // main loops dropped on ties (one per lane, by ticket), while the other
-        // waves finish theirs, so the re-traces fill the frame's tail.  A lane
-        // waits on an entry only while some wave of the grid is still in its
-        // main loop (the list is final once every wave is past it); a wave that
-        // sees nothing change for kRedoPatience leaves its tickets to k_redo --
-        // also the way out if the dispatcher held blocks back behind resident
-        // ones.  (Counting started waves instead of the grid cost 2 % in
-        // register allocation, measured.)
-        constexpr uint64_t kRedoPatience = 500000;  // s_memrealtime ticks (100 MHz): 5 ms
+        // waves finish theirs, so the re-traces fill the frame's tail.  The
+        // list is final by a completion count: a lane waits on an entry while
+        // some wave of the grid is still in its main loop (kRedoWaves < waves)
+        // and leaves once every wave is past it and no ticket below the list
+        // length is left.  The grid is the co-resident block count
+        // (occupancy_grid), so every wave reaches its redo phase and no entry
+        // is left to k_redo (stats redo_late = 0, asserted by the GPU suite).
+        // kRedoGuard is only a deadlock guard for a dispatcher that holds
+        // blocks back behind resident ones (the GPU shared with another
+        // process): after 250 ms in which neither the list nor the count of
+        // waves past their main loop changed, the wave leaves its tickets to
+        // k_redo.  A wave waits through the frame's tail only, and the count
+        // changes every time a wave leaves its main loop.  (Counting started waves instead of
+        // the grid cost 2 % in register allocation, measured.)
+        constexpr uint64_t kRedoGuard = 25000000;  // s_memrealtime ticks (100 MHz): 250 ms
         const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
         // pc.redo_lanes lanes of the wave take tickets: a re-trace is one
         // lane's whole path, so fewer per wave spread them over more waves
@@ -1811,7 +1818,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             if (sig != seen || since == 0) {
                 seen = sig;
                 since = now;
-            } else if (now - since > kRedoPatience) {
+            } else if (now - since > kRedoGuard) {
                 break;
             }
             __builtin_amdgcn_s_sleep(16);
