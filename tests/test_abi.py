@@ -92,13 +92,14 @@ def test_cli_usage_without_gpu():
 def test_product_library_reads_no_environment_knobs():
     """The library's control plane is the per-scene options API (tmpt.h "Scene
     options"); in the product build only the host's OBJ / PNG thread counts
-    come from the environment (the diagnostic TMPT_DIAG build adds traces)."""
+    come from the environment (the diagnostic TMPT_DIAG build adds traces, the
+    checked TMPT_CHECK build its self-test switch)."""
     csrc = os.path.join(ROOT, "toymeshpathtracer_amd", "csrc")
     names = set()
     for f in os.listdir(csrc):
         if f.endswith((".hip", ".cpp", ".h")):
             text = open(os.path.join(csrc, f)).read()
-            text = re.sub(r"#ifdef TMPT_DIAG.*?#endif", "", text, flags=re.S)
+            text = re.sub(r"#ifdef TMPT_(DIAG|CHECK)\b.*?#endif", "", text, flags=re.S)
             names |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', text))
             names |= set(re.findall(r'(?:env_int|host_threads)\("([A-Z_0-9]+)"', text))
     assert names <= {"TMPT_OBJ_THREADS", "TMPT_PNG_THREADS", "TMPT_OBJ_CHUNK", "TMPT_PNG_STRIP"}, names

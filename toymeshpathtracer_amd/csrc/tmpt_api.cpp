@@ -418,6 +418,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.rss_host) (void)hipHostFree(s.rss_host);
     if (s.wait_ev) (void)hipEventDestroy(s.wait_ev);
     if (s.counters) (void)hipFree(s.counters);
+    if (s.chk) (void)hipFree(s.chk);
     if (s.counters_host) (void)hipHostFree(s.counters_host);
     for (auto e : s.render_ev)
         if (e) (void)hipEventDestroy(e);
@@ -476,7 +477,7 @@ int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax
         (void)hipFree(d_refs);
         return -1;
     }
-    const OctView ov{d_nodes, d_refs, (int32_t)t.nodes.size(), n_flat, s.ties, grid};
+    const OctView ov{d_nodes, d_refs, (int32_t)t.nodes.size(), n_flat, s.ties, grid, (int64_t)t.refs.size()};
     if (hipMemcpy(s.oct_view, &ov, sizeof(ov), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d_nodes);
         (void)hipFree(d_refs);
@@ -611,6 +612,7 @@ int scene_hit(const tmpt_scene* hc, const float* rays, int64_t n, float tmin, fl
         s.root_misses = s.counters_host[kTieCounter + 1];
         s.crack_queries = s.counters_host[kCrackCounter];
     }
+    if (!rc) rc = check_report(s, "tmpt_scene_hit");
     cleanup();
     return rc;
 }
@@ -685,6 +687,7 @@ int tmpt_render(tmpt_scene* h, const tmpt_camera* cam, const tmpt_render_desc* d
     if (dev_out) d_out = (uint32_t*)rgba_out;
     else if (bytes && hipMalloc(&d_out, bytes) != hipSuccess) return bad("tmpt_render: out of device memory");
     int rc = render(s, cam, d, d_out, ray_count);
+    if (!rc) rc = check_report(s, "tmpt_render");
     if (!rc && !dev_out && bytes) {
         if (hipMemcpy(rgba_out, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess)
             rc = (set_error("tmpt_render: readback failed"), -1);

@@ -105,7 +105,20 @@ struct OctView {
     int32_t flat;  // triangles marked flat (0: the any-hit answers need no check)
     unsigned long long* ties;
     OctGrid grid;
+    int64_t n_refs;  // entries of refs (the checked build's bound)
 };
+
+// Device bounds checks, the checked build only (make CHECK=1: -DTMPT_CHECK,
+// ../_lib_check; tools/check_build.sh).  The traversal, both octree walks and
+// the hit-record loads test each index before they use it -- BVH node, leaf
+// range, stack depth, octree skip link and reference list, triangle id --
+// and a failed test ends that query and ORs its code into Scene::chk
+// ({codes, count, last offending value}); the API call then fails with
+// kCheckError and names the codes (tmpt_last_error).  The product build
+// compiles none of it.
+constexpr uint32_t kChkNode = 1u, kChkLeaf = 2u, kChkStack = 4u, kChkOctSkip = 8u, kChkOctRef = 16u,
+                   kChkTri = 32u;
+constexpr int kCheckError = -30;
 
 struct OctreeHost {
     std::vector<OctNode> nodes;
@@ -241,6 +254,7 @@ struct Scene {
     hipEvent_t wait_ev = nullptr;  // TMPT_FLAG_WAIT_STREAM: reused across renders
     unsigned long long* counters = nullptr;       // a render's ray / visit counters (device)
     unsigned long long* counters_host = nullptr;  // their pinned host copy
+    uint32_t* chk = nullptr;  // the checked build's device word triple (kChk* codes), else unused
     hipEvent_t render_ev[2] = {nullptr, nullptr}; // first / last kernel of a render
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
@@ -318,6 +332,7 @@ int build_soa(Scene& s);  // layout=soa planes from the built AoS records
 int mark_flat_triangles(Scene& s, const std::vector<uint8_t>& flat);
 // tmpt_render.hip: the scene's counters, pinned copy and render events (once)
 int ensure_counters(Scene& s);
+int check_report(Scene& s, const char* what);
 // tmpt_render.hip: sample_seed's byte tables for samples [0, spp) (1024 words each)
 void sample_jump_tables(int32_t spp, std::vector<uint32_t>& tab);
 // device radix sort of (key, value) pairs (tmpt_bvh.hip); returns 0 if the

@@ -208,7 +208,7 @@ __device__ __forceinline__ int rlane(int v, int l) { return __builtin_amdgcn_rea
 // tools/ diag TMPT_EXP_WALKSTAT, profiles/r04_ties/walkstat_n1.log).
 __device__ __forceinline__ OctHit octree_walk_wave(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
                                                    int n_oct, const TriOrig* __restrict__ tris, f3 o, f3 d,
-                                                   float tmin, float tmax, float target)
+                                                   float tmin, float tmax, float target TMPT_CHK_PARAMS)
 {
     const f3 inv = ref_inverse(d);
     const int lane = lane_id();
@@ -230,11 +230,14 @@ __device__ __forceinline__ OctHit octree_walk_wave(const OctNode* __restrict__ n
         while (cur < end) {
             const int k = cur - i;
             if (((P >> k) & 1ull) == 0) {
-                cur = rlane(skip, k);
+                const int sk = rlane(skip, k);
+                if (TMPT_CHK(chk, sk > cur && sk <= n_oct, kChkOctSkip, sk)) return h;
+                cur = sk;
                 continue;
             }
             if ((L >> k) & 1ull) {
                 const int r = rlane(ref, k);
+                if (TMPT_CHK(chk, (int64_t)r < n_refs && (int64_t)r + refs[r] < n_refs, kChkOctRef, r)) return h;
                 const int cnt = refs[r];
                 for (int b = 0; b < cnt; b += 64) {
                     float t = INFINITY, u = 0.0f, v = 0.0f;
@@ -242,6 +245,7 @@ __device__ __forceinline__ OctHit octree_walk_wave(const OctNode* __restrict__ n
                     bool ok = false;
                     if (b + lane < cnt) {
                         id = refs[r + 1 + b + lane];
+                        if (TMPT_CHK(chk, (uint32_t)id < (uint32_t)n_tri, kChkTri, id)) id = 0;
                         const float4* p = reinterpret_cast<const float4*>(tris + id);
                         const float4 a = p[0], bb = p[1], c = p[2];
                         const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, bb.x, bb.y), v2 = mk(bb.z, bb.w, c.x);
@@ -1407,7 +1411,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const f3 qo = mk(rlane(r.o.x, l), rlane(r.o.y, l), rlane(r.o.z, l));
                         const f3 qd = mk(rlane(r.d.x, l), rlane(r.d.y, l), rlane(r.d.z, l));
                         const OctHit h = octree_walk_wave(ov->nodes, ov->refs, ov->n, sv.tri_orig, qo, qd, kMinT, kMaxT,
-                                                          rlane(qany ? -INFINITY : ts.bt, l));
+                                                          rlane(qany ? -INFINITY : ts.bt, l) TMPT_CHK_ARGS(sv));
                         if (lane_id() == l) {
                             octree_count(ov, ts.best);
                             ts.best = h.best;
@@ -2319,6 +2323,14 @@ SceneView view(const Scene& s)
 {
     SceneView v{s.nodes4, s.tri_pre, s.tri_orig, s.n, s.n_nodes4};
     v.soa = s.soa;
+#ifdef TMPT_CHECK
+    v.chk = s.chk;
+    // TMPT_CHECK_SELFTEST=1 (the report's own test, tests/test_gpu_check.py):
+    // the view claims a single BVH node, so every query that descends past
+    // the root fails the node test
+    if (const char* e = getenv("TMPT_CHECK_SELFTEST"))
+        if (atoi(e) == 1) v.n_nodes4 = std::min(v.n_nodes4, 1);
+#endif
     if (s.oct && s.opt.tie_rule == 0) {  // the reference's visit order for ties
         v.oct = s.oct_view;
         const OctGrid& g = s.oct_grid;
@@ -3568,7 +3580,39 @@ int ensure_counters(Scene& s)
                            hipHostMallocDefault));
     for (auto& e : s.render_ev) TMPT_HIP(hipEventCreate(&e));
     s.ties = s.counters + kTieCounter;
+#ifdef TMPT_CHECK
+    TMPT_HIP(hipMalloc(&s.chk, 4 * sizeof(uint32_t)));
+    TMPT_HIP(hipMemset(s.chk, 0, 4 * sizeof(uint32_t)));
+#endif
     return 0;
+}
+
+// The checked build's report (tmpt_internal.h kChk*): after a call's kernels
+// are done, kCheckError with the codes, the count and the last offending
+// value when any index test failed (the word triple is cleared for the next
+// call); 0 otherwise, and always 0 in the product build.
+int check_report(Scene& s, const char* what)
+{
+#ifdef TMPT_CHECK
+    if (!s.chk) return 0;
+    uint32_t h[3] = {0, 0, 0};
+    TMPT_HIP(hipDeviceSynchronize());
+    TMPT_HIP(hipMemcpy(h, s.chk, sizeof(h), hipMemcpyDeviceToHost));
+    if (h[0] == 0) return 0;
+    TMPT_HIP(hipMemset(s.chk, 0, 4 * sizeof(uint32_t)));
+    char msg[256];
+    snprintf(msg, sizeof(msg),
+             "%s: device index check failed: codes 0x%x (1 node, 2 leaf, 4 stack, 8 octree skip, 16 octree refs, "
+             "32 triangle id), %u times, last value %d",
+             what, h[0], h[1], (int)h[2]);
+    fprintf(stderr, "tmpt: %s\n", msg);
+    set_error(msg);
+    return kCheckError;
+#else
+    (void)s;
+    (void)what;
+    return 0;
+#endif
 }
 
 int intersect_batch(Scene& s, const float* d_rays, int64_t n, float tmin, float tmax, bool any, bool ranged,

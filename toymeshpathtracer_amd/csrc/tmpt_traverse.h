@@ -145,7 +145,30 @@ struct SceneView {
     // build option layout=soa (tmpt_internal.h SoaScene): the same nodes and
     // triangle records as planes, read by the SOA instantiations
     SoaScene soa;
+#ifdef TMPT_CHECK
+    uint32_t* chk = nullptr;  // Scene::chk (tmpt_internal.h kChk*)
+#endif
 };
+
+// TMPT_CHK(chk, ok, code, what): in the checked build, true (and `code`
+// recorded) when `ok` fails, so the caller can end the query before the bad
+// access; in the product build a constant false that evaluates nothing.
+#ifdef TMPT_CHECK
+__device__ __noinline__ void chk_fail(uint32_t* chk, uint32_t code, int what)
+{
+    if (chk == nullptr) return;
+    __hip_atomic_fetch_or(&chk[0], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&chk[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&chk[2], (uint32_t)what, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define TMPT_CHK(chk, ok, code, what) (__builtin_expect(!(ok), 0) && (chk_fail((chk), (code), (int)(what)), true))
+#define TMPT_CHK_PARAMS , uint32_t *chk, int64_t n_refs, int32_t n_tri
+#define TMPT_CHK_ARGS(sv) , (sv).chk, (sv).oct->n_refs, (sv).n
+#else
+#define TMPT_CHK(chk, ok, code, what) false
+#define TMPT_CHK_PARAMS
+#define TMPT_CHK_ARGS(sv)
+#endif
 
 struct TravCount {
     uint32_t nodes = 0, tris = 0;
@@ -201,6 +224,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
     // KIND 1 / 2: the caller guarantees the lane is at a node / at a leaf (a
     // voted round), so the other kind's code is not emitted at all
     if (KIND == 1 || (KIND == 0 && ts.node >= 0)) {
+        if (TMPT_CHK(sv.chk, (uint32_t)ts.node < (uint32_t)sv.n_nodes4, kChkNode, ts.node)) return true;
         // 32-bit byte offset off an SGPR base: one VALU for the address
         uint4 A, B, C;
         int4 L;
@@ -270,6 +294,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             const float kn = sab ? kb : ka, kno = sab ? ka : kb;
             const int cn = sab ? cb : ca, cno = sab ? ca : cb;
             if (kn != INFINITY) {
+                if (TMPT_CHK(sv.chk, ts.sp + 3 <= kStackTotal, kChkStack, ts.sp)) return true;
                 st.push3(ts.sp, kbo != INFINITY, cbo, kao != INFINITY, cao, kno != INFINITY, cno);
                 ts.node = cn;
                 return false;
@@ -280,6 +305,8 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
         const uint32_t code = (uint32_t)ts.node;
         const uint32_t first = code & kLeafFirstMask;
         const uint32_t n = ((code >> kLeafCountShift) & 15u) + 1u;
+        // records [0, n] (record n: the null leaf's)
+        if (TMPT_CHK(sv.chk, first + n <= (uint32_t)sv.n + 1u, kChkLeaf, code)) return true;
         const char* base = reinterpret_cast<const char*>(sv.tri_pre);
         // Accepts (t, u, v, id) by the closest-hit order; true = any-hit query done.
         auto tri = [&](const float4& a, const float4& b, const float4& c) -> bool {
@@ -453,7 +480,7 @@ struct OctHit {
 
 __device__ __forceinline__ OctHit octree_walk(const OctNode* __restrict__ nodes, const int32_t* __restrict__ refs,
                                                int n_oct, const TriOrig* __restrict__ tris, f3 o, f3 d,
-                                               float tmin, float tmax, float target)
+                                               float tmin, float tmax, float target TMPT_CHK_PARAMS)
 {
     const f3 inv = ref_inverse(d);
     OctHit h{-1, tmax, 0.0f, 0.0f};
@@ -466,14 +493,18 @@ __device__ __forceinline__ OctHit octree_walk(const OctNode* __restrict__ nodes,
 #endif
         const float4 lo = nodes[i].lo, hi = nodes[i].hi;
         if (!ref_slab(o, inv, lo, hi, tmin, tmax)) {
-            i = __float_as_int(lo.w);
+            const int skip = __float_as_int(lo.w);
+            if (TMPT_CHK(chk, skip > i && skip <= n_oct, kChkOctSkip, skip)) break;
+            i = skip;
             continue;
         }
         const int ref = __float_as_int(hi.w);
         if (ref >= 0) {
+            if (TMPT_CHK(chk, (int64_t)ref < n_refs && (int64_t)ref + refs[ref] < n_refs, kChkOctRef, ref)) break;
             const int cnt = refs[ref];
             for (int k = 1; k <= cnt; ++k) {
                 const int id = refs[ref + k];
+                if (TMPT_CHK(chk, (uint32_t)id < (uint32_t)n_tri, kChkTri, id)) continue;
                 const float4* p = reinterpret_cast<const float4*>(tris + id);
                 const float4 a = p[0], b = p[1], c = p[2];
                 const f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
@@ -505,7 +536,8 @@ __device__ __forceinline__ OctHit octree_walk(const OctNode* __restrict__ nodes,
 __device__ __forceinline__ int octree_closest(const SceneView& sv, f3 o, f3 d, float tmin, float tmax, float target,
                                               float& bt, float& bu, float& bv)
 {
-    const OctHit h = octree_walk(sv.oct->nodes, sv.oct->refs, sv.oct->n, sv.tri_orig, o, d, tmin, tmax, target);
+    const OctHit h =
+        octree_walk(sv.oct->nodes, sv.oct->refs, sv.oct->n, sv.tri_orig, o, d, tmin, tmax, target TMPT_CHK_ARGS(sv));
     bt = h.t;
     bu = h.u;
     bv = h.v;
@@ -650,6 +682,7 @@ __device__ __forceinline__ int traverse(const SceneView& sv, const TravRay& r, f
 __device__ __forceinline__ void hit_record(const SceneView& sv, int id, float u, float v, f3& pos,
                                            f3& nrm)
 {
+    if (TMPT_CHK(sv.chk, (uint32_t)id < (uint32_t)max(sv.n, 1), kChkTri, id)) id = 0;
     const float4* p = reinterpret_cast<const float4*>(sv.tri_orig + id);
     float4 a = p[0], b = p[1], c = p[2];
     f3 v0 = mk(a.x, a.y, a.z), v1 = mk(a.w, b.x, b.y), v2 = mk(b.z, b.w, c.x);
