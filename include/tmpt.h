@@ -3,7 +3,9 @@
  * pr0g/ToyMeshPathTracer: Trace() -> Scatter() -> Scene::HitScene().
  *
  * Plain C: opaque handles, plain pointers and sizes, int status codes
- * (0 = ok, < 0 = error; message in tmpt_last_error()), no C++ exceptions and no
+ * (0 = ok, < 0 = error; message in tmpt_last_error(); -30 only from the
+ * checked build, make CHECK=1: a device index test failed during the call),
+ * no C++ exceptions and no
  * torch types cross this boundary.  Every entry point names the reference
  * interface it replaces (/root/reference/source/<file>:<line>); INTEGRATION.md
  * shows the reference-side binding.
