@@ -5,7 +5,9 @@ tools/_bin/base from an earlier commit), alternating, on the bench frame.
   python tools/ab_kpath.py <pkgdir_a>[:opts],<pkgdir_b>[:opts][,...] [frames] [loads]
   opts: scene build options with ';' between them, e.g. .:split=20;leaf_max=4
   loads: comma list of seed:shards, e.g. sample:1,sample:8,pixel:1
-Prints per load the median k_path ms (tmpt_stats.extend_ms) of each build."""
+Prints per load the median k_path ms (tmpt_stats.extend_ms) of each build.
+AB_RES=3840x2160 AB_SPP=256 select another frame of the stand-in sponza (configs[4]);
+AB_TIME=render times the whole render (every kernel of the call) instead of k_path."""
 import json
 import os
 import subprocess
@@ -21,7 +23,7 @@ import toymeshpathtracer_amd as tm
 import gen_standin_sponza
 frames = int(sys.argv[3]); loads = sys.argv[4].split(",")
 tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
-w, h, spp = 1920, 1080, 64
+w, h = map(int, os.environ.get("AB_RES", "1920x1080").split("x")); spp = int(os.environ.get("AB_SPP", "64"))
 cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
 seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL, "row": tm.SEED_ROW}
 out = {}
@@ -32,7 +34,8 @@ with tm.Scene(tris, bounds=(bmin, bmax), options=opts.replace(";", ",") or None)
         for i in range(frames + 1):
             sc.trace_image(cam, w, h, spp, seed_mode=seeds[sd], band_rows=1, shard=n - 1, num_shards=n)
             # row seeding runs several kernels: the render's whole device time
-            if i: ms.append(sc.stats().render_ms if sd == "row" else sc.stats().extend_ms)
+            if i: ms.append(sc.stats().render_ms if sd == "row" or os.environ.get("AB_TIME") == "render"
+                            else sc.stats().extend_ms)
         out[ld] = statistics.median(ms)
 print(json.dumps(out))
 '''
