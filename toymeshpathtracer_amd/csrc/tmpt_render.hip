@@ -2763,10 +2763,14 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // other lanes' shadow queries, and (ordered passes) each 64-rank chunk pairs
     // `pair` expensive ranks with 64-pair cheap ones, whose lanes free up early.
     // Bench frame: 1/4 shard 86.4 -> 77.2 ms (pair 56), 1/8 shard 45.7 -> 43.9 ms
-    // (pair 52); at 1/2 and 1/1 it loses (the extra shading code), so it is off
-    // there.  Options help and pair override the choice.
+    // (pair 52).  Re-measured in round 5 as whole renders (help on / off,
+    // profiles/r05_experiments/*_help.log): 1080p N=1 214.4 / 210.6 ms, 1/2
+    // 116.6 / 120.6, 1/4 63.9 / 75.5, 1/8 36.4 / 38.8; 4K x 256 1/2 1599.6 /
+    // 1531.5, 1/4 838.6 / 814.5, 1/8 450.3 / 467.9 -- it wins up to ~4 pixels
+    // per resident lane and loses from ~8 (the extra shading code), so it is
+    // on at <= 4.5.  Options help and pair override the choice.
     const int64_t lanes = (int64_t)grid * kBlk;
-    int help = ordered && fn == fn_default && 2 * P <= 5 * lanes ? 1 : 0;
+    int help = ordered && fn == fn_default && 2 * P <= 9 * lanes ? 1 : 0;
     if (o.help >= 0) help = o.help != 0 && !count && !prof && !a.jt;
     const uint32_t oct_shadow = oct_shadow_check(s);
     if (oct_shadow) help = 0;  // the helpers' shadow answers are not checked
