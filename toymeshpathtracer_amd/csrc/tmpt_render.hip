@@ -190,6 +190,9 @@ __device__ __forceinline__ uint32_t render_pixel(const SceneView& sv, const Rend
 #ifdef TMPT_EXP_WALKSTAT
 __device__ unsigned long long g_walkstat[4];
 #endif
+#ifdef TMPT_EXP_CRACKSTAT
+__device__ unsigned long long g_crackstat[4];
+#endif
 
 // ============================================================ octree walk, one wave
 __device__ __forceinline__ float rlane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
@@ -3788,6 +3791,18 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.tie_queries = c[kTieCounter];
     s.root_misses = c[kTieCounter + 1];
     s.crack_queries = c[kCrackCounter];
+#ifdef TMPT_EXP_CRACKSTAT
+    {
+        unsigned long long w[4] = {0, 0, 0, 0};
+        if (hipMemcpyFromSymbol(w, HIP_SYMBOL(g_crackstat), sizeof(w)) == hipSuccess && w[0]) {
+            fprintf(stderr, "crack test: %llu finished hits, first stage true %llu (%.3f %%), both stages %llu, "
+                            "t < reach %llu (%.3f %%)\n",
+                    w[0], w[1], 100.0 * w[1] / w[0], w[2], w[3], 100.0 * w[3] / w[0]);
+            const unsigned long long z[4] = {0, 0, 0, 0};
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_crackstat), z, sizeof(z));
+        }
+    }
+#endif
 #ifdef TMPT_EXP_WALKSTAT
     {
         unsigned long long w[4] = {0, 0, 0, 0};

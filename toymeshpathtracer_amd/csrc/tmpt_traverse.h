@@ -592,6 +592,17 @@ __device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& 
     const float span = fminf(ts.bt, sv.crack.x);
     const bool ax = fabsf(r.d.x) * span <= sv.crack.y, ay = fabsf(r.d.y) * span <= sv.crack.z,
                az = fabsf(r.d.z) * span <= sv.crack.w;
+#ifdef TMPT_EXP_CRACKSTAT  // cost experiment: how often each stage runs and fires
+    {
+        extern __device__ unsigned long long g_crackstat[4];
+        const bool s2 = (ax | ay | az) && octree_crack_planes(sv.oct->grid, r.o, r.d, ts.bt, ax, ay, az);
+        atomicAdd(&g_crackstat[0], 1ull);
+        if (ax | ay | az) atomicAdd(&g_crackstat[1], 1ull);
+        if (s2) atomicAdd(&g_crackstat[2], 1ull);
+        if (ts.bt < sv.crack.x) atomicAdd(&g_crackstat[3], 1ull);
+        return s2;
+    }
+#endif
     return (ax | ay | az) && octree_crack_planes(sv.oct->grid, r.o, r.d, ts.bt, ax, ay, az);
 #endif
 }
