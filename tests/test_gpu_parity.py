@@ -856,6 +856,31 @@ def test_sample_mode_matches_oracle(gpu, engine, name, w, h, spp):
     sc.close()
 
 
+@pytest.mark.parametrize("octree", [False, True])
+def test_sample_mode_tail_units(gpu, octree):
+    """Sample seeding's tail (option sample_tail): the last blocks are handed
+    out as single-sample units.  With blocks of 2 and one tail block per
+    resident lane the frame mixes both kinds of unit; it equals the oracle
+    and the render without a tail (every block a unit), with the octree's
+    deferred ties too; the whole frame as single units as well."""
+    tris, bmin, bmax, sc = _scene("teapot.obj", octree=octree)
+    w, h, spp = 320, 180, 16
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    osc = _ref_oracle(tris, bmin, bmax) if octree else \
+        oracle.Scene(tris, accel=oracle.ACCEL_BVH, tie=oracle.TIE_INDEX, bmin=bmin, bmax=bmax)
+    ref, ref_rays = osc.render(cam.as_array(), w, h, spp, seed_mode=oracle.SEED_SAMPLE)
+    sc.set_option("sample_block", 2)
+    if octree:
+        sc.set_option("tie_defer", 1)
+    for tail in (0, 1, 64):  # none; 262 k of 460,800 blocks (mixed); every block
+        sc.set_option("sample_tail", tail)
+        img, rays = sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE)
+        assert rays == ref_rays, tail
+        diff = np.nonzero((img != ref).any(-1))
+        assert diff[0].size == 0, f"tail {tail}: {diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
+    sc.close()
+
+
 def test_sample_mode_shards_and_sizes(gpu, monkeypatch):
     """Sample seeding: 1-row bands over 3 and 8 shards reassemble to the
     1-shard frame with the same ray count (auto block size differs per

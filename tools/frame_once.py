@@ -1,7 +1,7 @@
 """One bench frame (stand-in sponza 1920x1080x64, the reference octree built)
 per seeding mode given, for experiment builds that print their own
 statistics (TMPT_LIB_PATH=<variant>/libtmpt.so).
-  python tools/frame_once.py [sample,pixel,row] [shards]"""
+  python tools/frame_once.py [sample,pixel,row] [shards] [options, e.g. "sample_tail=8,redo_lanes=16"]"""
 import os
 import sys
 
@@ -16,7 +16,8 @@ shards = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 seeds = {"sample": tm.SEED_SAMPLE, "pixel": tm.SEED_PIXEL, "row": tm.SEED_ROW}
 tris, bmin, bmax = tm.load_scene(gen_standin_sponza.ensure())
 cam = tm.Camera.for_scene(bmin, bmax, 1920, 1080, is_sponza=True)
-with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+opts = sys.argv[3] if len(sys.argv) > 3 else None
+with tm.Scene(tris, bounds=(bmin, bmax), options=opts) as sc:
     for m in modes:
         _, rays = sc.trace_image(cam, 1920, 1080, 64, seed_mode=seeds[m], band_rows=1, num_shards=shards)
         st = sc.stats()

@@ -193,6 +193,10 @@ __device__ unsigned long long g_walkstat[4];
 #ifdef TMPT_EXP_CRACKSTAT
 __device__ unsigned long long g_crackstat[4];
 #endif
+#ifdef TMPT_EXP_WAVETIME  // timeline experiment: per wave, s_memrealtime at start / main loop end / exit
+constexpr int kWaveTimeMax = 16384;
+__device__ unsigned long long g_wavetime[3 * kWaveTimeMax];
+#endif
 
 // ============================================================ octree walk, one wave
 __device__ __forceinline__ float rlane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
@@ -881,6 +885,10 @@ struct PathCtl {
     // and k_resolve sums them in sample order (main.cpp:218's col += Trace).
     uint32_t nblk, blk;
     uint32_t blk0;  // progressive pass: the block of its first sample (units = the pass's blocks)
+    // the frame's tail (option sample_tail): units >= ua are single samples,
+    // unit ua + v = sample v % blk of block ua + v / blk, so the last units
+    // handed out are one sample long, not one block
+    uint32_t ua;
     float4* __restrict__ sbuf;
     uint32_t sb_ss, sb_sp;  // sbuf index = sample * sb_ss + pixel * sb_sp ([pixel][sample]: 1, spp)
     uint32_t pair;          // sample pairs (2k, 2k+1) of a unit written back to back (one 32-B sector)
@@ -1184,6 +1192,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         if (res >= res_end)
             for (int k = 0; k < 6; ++k) __builtin_amdgcn_s_sleep(127);
     }
+#ifdef TMPT_EXP_WAVETIME
+    const int wt_id = (int)(gtid >> 6);
+    if (lane_id() == 0 && wt_id < kWaveTimeMax) g_wavetime[3 * wt_id] = __builtin_amdgcn_s_memrealtime();
+#endif
     bool has_pix = false, in_query = false, qany = false;
     // HELP (shadow offload to idle lanes): once the pixel supply is exhausted, a
     // lane without a pixel becomes a helper that traces another lane's shadow
@@ -1203,6 +1215,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0, pf_smp = 0xFFFFFFFFu, pf_pix = 0;
     // SAMP 2: the unit held, the ray counts at its start, the camera's RNG draws
     uint32_t cur_unit = 0, re0 = 0, rs0 = 0, ndraw = 0;
+    bool single = false;  // SAMP 1: the unit is one sample of the frame's tail (PathCtl::ua)
     uint32_t psteps = 0;  // traversal steps of this pixel in this call (pc.cost_out)
     // COUNT: wave-uniform round statistics (node/leaf rounds and their stepping
     // lanes, shading rounds, lanes wanting shading, lanes traversing meanwhile)
@@ -1351,8 +1364,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         rs0 = rays_s;
                     } else if (SAMP && pc.nblk > 1) {  // sample seeding: (pixel, block) units
                         const uint32_t unit = res + k;
-                        pix = unit / pc.nblk;
-                        smp0 = (unit - pix * pc.nblk + pc.blk0) * pc.blk;  // blk0: a progressive pass's first block
+                        uint32_t q = unit, sub = 0u;  // block, sample within it (tail units)
+                        single = unit >= pc.ua;
+                        if (single) {
+                            const uint32_t v = unit - pc.ua, qv = v / pc.blk;
+                            q = pc.ua + qv;
+                            sub = v - qv * pc.blk;
+                        }
+                        pix = q / pc.nblk;
+                        smp0 = (q - pix * pc.nblk + pc.blk0) * pc.blk + sub;  // blk0: a progressive pass's first block
                     } else {
                         pix = (kFull && pc.order) ? pc.order[res + k] : res + k;
                     }
@@ -1611,12 +1631,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
 #ifdef TMPT_EXP_NOPAIR  // cost experiment: no paired stores
                         if (false) {
 #else
-                        if (pc.pair && !odd && smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u) {
+                        if (pc.pair && !odd && !single && smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u) {
 #endif
                             col = color;
                         } else {
                             // DEFER: a dropped sample's slot (x = -1) is redo_sample's
-                            if (pc.pair && odd && (!DEFER || !(col.x < 0.0f)))
+                            if (pc.pair && odd && !single && (!DEFER || !(col.x < 0.0f)))
                                 __builtin_nontemporal_store((f32x4){col.x, col.y, col.z, 0.0f}, dst - 1);
                             if (!DEFER || !(color.x < 0.0f))
                                 __builtin_nontemporal_store((f32x4){color.x, color.y, color.z, 0.0f}, dst);
@@ -1625,7 +1645,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         col = col + color;
                     ++smp;
                     depth = 0;
-                    if (smp < (uint32_t)a.smp_end && (!SAMP || (smp & a.bmask) != 0u)) {
+                    if (smp < (uint32_t)a.smp_end && (!SAMP || ((smp & a.bmask) != 0u && !single))) {
                         cam = true;
                     } else {
                         if (kFull && a.prog) a.prog[pix] = make_float4(col.x, col.y, col.z, __uint_as_float(rng));
@@ -1649,7 +1669,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     rng = (pf_smp == smp && pf_pix == pix) ? (pf0 ^ pf1 ^ pf2 ^ pf3) : sample_seed(a.jt, smp, ps);
                     // the block's next sample: its table words now, XORed at its start
                     const uint32_t* t = a.jt + (size_t)(smp + 1u) * 1024u;
-                    const bool more = smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u;
+                    const bool more = smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u && !single;
                     const uint32_t* tt = more ? t : a.jt;
                     pf0 = tt[ps & 255u];
                     pf1 = tt[256u + ((ps >> 8) & 255u)];
@@ -1768,6 +1788,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             }
         }
     }
+#ifdef TMPT_EXP_WAVETIME
+    if (lane_id() == 0 && wt_id < kWaveTimeMax) g_wavetime[3 * wt_id + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (DEFER && pc.redo_inline) {
         // Redo phase: the wave's main loop is over; it traces the samples the
         // main loops dropped on ties (one per lane, by ticket), while the other
@@ -1831,6 +1854,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             __builtin_amdgcn_s_sleep(16);
         }
     }
+#ifdef TMPT_EXP_WAVETIME
+    if (lane_id() == 0 && wt_id < kWaveTimeMax) g_wavetime[3 * wt_id + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (SAMP == 4 && lane_id() == 0) {
         atomicAdd(&pc.rss.ctl[5], n_claim);
         atomicAdd(&pc.rss.ctl[6], n_miss);
@@ -2744,7 +2770,27 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             }
         }
     }
-    const int64_t P = a.slots * (int64_t)nblk;  // units the supply hands out
+    int64_t P = a.slots * (int64_t)nblk;  // units the supply hands out
+    // Sample seeding's tail (option sample_tail): the last sample_tail blocks
+    // per resident lane are handed out as single samples, so a lane's last
+    // unit is one sample, not a block of blk, and the waves leave their main
+    // loops closer together: bench frame, N=1, blocks of 8, the main loops
+    // ended over 8.6 ms without it and over 1.7 ms with 8 blocks per lane
+    // (profiles/r05_wavetime/; the deferred re-traces are then the last
+    // ~2 ms).  k_path, tail 0 / 8 blocks per lane: N=1 188.0 / 186.0 ms, 1/2
+    // 96.1 / 94.7 ms (16: slower again, the single units' own seed jumps;
+    // profiles/r05_experiments/sample_tail*.log).
+    uint32_t ua = 0xFFFFFFFFu;
+    // (only when every block is full: a partial last block would map tail
+    // units to samples past the pass's end)
+    if (a.jt && nblk > 1 && blk >= 2u && o.sample_tail > 0 && (s1 - s0) % blk == 0) {
+        int64_t nb = std::min<int64_t>(P, (int64_t)o.sample_tail * grid * kBlk);
+        while (nb > 0 && (P - nb) + nb * (int64_t)blk >= (1ll << 31)) nb /= 2;
+        if (nb > 0) {
+            ua = (uint32_t)(P - nb);
+            P = (P - nb) + nb * (int64_t)blk;
+        }
+    }
     // Pilot ordering (SURVEY §8e "pull tiles dynamically", at pixel grain): when
     // a shard has several pixels per resident lane, the frame ends with the
     // chains of the pixels started last.  A first pass runs `pilot` samples of
@@ -2800,6 +2846,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     pc.nblk = nblk;
     pc.blk = blk;
     pc.blk0 = blk0;
+    pc.ua = ua;
     RenderArgs as = a;  // sample seeding: a lane's run of samples is its block
     if (a.jt) {
         as.bmask = nblk > 1 ? blk - 1u : 2047u;
@@ -3791,6 +3838,34 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.tie_queries = c[kTieCounter];
     s.root_misses = c[kTieCounter + 1];
     s.crack_queries = c[kCrackCounter];
+#ifdef TMPT_EXP_WAVETIME
+    {
+        std::vector<unsigned long long> w(3 * kWaveTimeMax, 0ull);
+        if (hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wavetime), w.size() * 8) == hipSuccess) {
+            std::vector<double> st, ml, ex;
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < kWaveTimeMax; ++i)
+                if (w[3 * i] && w[3 * i + 2]) t0 = std::min(t0, w[3 * i]);
+            for (int i = 0; i < kWaveTimeMax; ++i)
+                if (w[3 * i] && w[3 * i + 2]) {
+                    st.push_back((w[3 * i] - t0) * 0.01);  // 100 MHz ticks -> us
+                    ml.push_back((w[3 * i + 1] - t0) * 0.01);
+                    ex.push_back((w[3 * i + 2] - t0) * 0.01);
+                }
+            auto pct = [](std::vector<double> v, double q) {
+                if (v.empty()) return 0.0;
+                std::sort(v.begin(), v.end());
+                return v[std::min(v.size() - 1, (size_t)(q * (v.size() - 1)))];
+            };
+            fprintf(stderr, "waves %zu; start us p0/p50/p100 %.0f/%.0f/%.0f; main loop end p0/p10/p50/p90/p100 "
+                            "%.0f/%.0f/%.0f/%.0f/%.0f; exit p0/p50/p99/p100 %.0f/%.0f/%.0f/%.0f\n",
+                    st.size(), pct(st, 0), pct(st, 0.5), pct(st, 1), pct(ml, 0), pct(ml, 0.1), pct(ml, 0.5),
+                    pct(ml, 0.9), pct(ml, 1), pct(ex, 0), pct(ex, 0.5), pct(ex, 0.99), pct(ex, 1));
+            std::fill(w.begin(), w.end(), 0ull);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wavetime), w.data(), w.size() * 8);
+        }
+    }
+#endif
 #ifdef TMPT_EXP_CRACKSTAT
     {
         unsigned long long w[4] = {0, 0, 0, 0};
