@@ -206,7 +206,7 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   help, pair       pixel seeding: shadow offload to idle lanes (-1 = auto, 0, 1)
  *                    and expensive ranks per 64-rank chunk (-1 = auto, 0..63)
  *   balance, dprio   pixel seeding: SIMD-balanced first chunks (1), longest-
- *                    remaining-first wave priority with offload (1)
+ *                    remaining-first wave priority in cost-ordered passes (1)
  *   wave_cap         pixel seeding: pixels a wave holds at once (0 = auto, 1..64)
  *   pixel_chains     pixel seeding, cost-ordered: the heaviest pixels per 1024 that run as
  *                    speculative chains (every even RNG offset past the pilot traced,

@@ -3054,14 +3054,21 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         pc.claim = simd_reg + 2 * (size_t)kSimdKeys + 64;
         TMPT_HIP(hipMemsetAsync(simd_reg, 0, reg_words * 4, s.stream));
     }
-    // Dynamic priority (PathCtl::dprio) at low load (with the helpers): the
-    // heaviest waves start at the top level and step down as their projected
-    // remaining work falls below 32 / 21 / 10.5 % of the heaviest pixel's, so
-    // the issue slots go to the waves with the most work left instead of to
-    // the oldest.  Bench frame, 1/8 shard 44.9 -> 42.4 ms, 1/4 78.9 -> 75.3 ms
-    // (with the balanced first chunks); at one pixel pass per lane or more it
-    // costs ~0.4 %, so it is off there.  Option dprio.
-    if (help && o.dprio) {
+    // Dynamic priority (PathCtl::dprio) in cost-ordered passes of up to ~12
+    // pixels per resident lane: the heaviest waves start at the top level and
+    // step down as their projected remaining work falls below 32 / 21 / 10.5 %
+    // of the heaviest pixel's, so the issue slots go to the waves with the
+    // most work left instead of to the oldest.  Bench frame, 1/8 shard 44.9 ->
+    // 42.4 ms, 1/4 78.9 -> 75.3 ms (with the balanced first chunks; rounds
+    // 1-2).  It was on only with the helpers until round 5, which measured it
+    // without them (whole renders, on / off, profiles/r05_experiments/dprio_*):
+    // 1080p N=1 207.1 / 209.8 ms (7.9 pixels per lane: the pass ends over
+    // ~24 ms as the last pixels' 64-sample chains run out,
+    // profiles/r05_wavetime/), 4K x 256 1/4 807.5 / 820.9 (7.9 per lane), but
+    // 1/2 1550.4 / 1528.5 and N=1 3023.4 / 2969.0 (15.8 and 31.6 per lane: the
+    // tail is short against the pass and the priority's own cost shows).
+    // Option dprio.
+    if (ordered && o.dprio && P <= 12 * lanes) {
         pc.dprio[0] = 0.32f;
         pc.dprio[1] = 0.21f;
         pc.dprio[2] = 0.105f;
