@@ -214,7 +214,7 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *   rowspec          row seeding on the persistent engine: 1 = speculative row
  *                    engine, 0 = one lane per row chain
  *   rowspec_wmax, rowspec_windows, rowspec_spread, rowspec_groups,
- *   rowspec_noshadow, rowspec_chase, rowspec_stream
+ *   rowspec_noshadow, rowspec_chase, rowspec_stream, rowstream_dynamic
  *                    speculative row engine: units per window (0 = auto),
  *                    windows per row and iteration (0 = auto, 1..32), window
  *                    spread in pixels (-1 = auto), row groups/streams (1..8),
@@ -222,7 +222,9 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    chase over LDS-staged units, one wave per row (1), the
  *                    streaming engine: one launch, chains walked on the device
  *                    as units finish (1, the default; 0 = host-driven iterations,
- *                    also the fallback when the streaming engine does not apply)
+ *                    also the fallback when the streaming engine does not apply),
+ *                    its windows and spread following the rows still chasing
+ *                    (1; 0 = fixed at the launch's load)
  *   rowstream_test_abort  test hook (0): 1 makes the streaming engine's chaser
  *                    blocks leave at once, so its watchdog (~2 ms then, ~1 s
  *                    normally) aborts the launch and the iterated engine renders

@@ -186,6 +186,7 @@ struct Options {
     float sah_c_leaf = 0.7f, sah_c_tri = 0.5f;  // SAH collapse costs (inner node = 1)
     // render (tmpt_scene_set_option)
     int sample_block = 0;     // sample seeding: samples per work unit, a power of two (0 = auto)
+    int rowstream_dynamic = 1;  // row seeding, streaming: windows and spread follow the live rows
     int sample_tail = 8;      // sample seeding: blocks per resident lane run as single samples at the end
     double sbuf_max = 0.0;    // sample seeding: cap on the per-sample colour buffer, bytes (0 = 3/4 of free HBM)
     int sbuf_pair = 1;        // sample seeding: a unit's sample pairs written back to back into one 32-B sector

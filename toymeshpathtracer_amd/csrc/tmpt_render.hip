@@ -196,6 +196,7 @@ __device__ unsigned long long g_crackstat[4];
 #ifdef TMPT_EXP_WAVETIME  // timeline experiment: per wave, s_memrealtime at start / main loop end / exit
 constexpr int kWaveTimeMax = 16384;
 __device__ unsigned long long g_wavetime[3 * kWaveTimeMax];
+__device__ unsigned long long g_rowtime[kWaveTimeMax];  // streaming row engine: when each row's chain ended
 #endif
 
 // ============================================================ octree walk, one wave
@@ -823,7 +824,11 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 //   list[(row * W + x) * spp + k] = offset of sample k of pixel x on the chain
 //   ctl: [0] rows done, [1] abort, [2] chain progress ticks, [3] error, [4] P,
 //        [5..11] statistics, [12] block arrival tickets (the first nchase are chasers)
-constexpr int kRssT = 8;
+#ifndef TMPT_RSS_T
+#define TMPT_RSS_T 8
+#endif
+constexpr int kRssT = TMPT_RSS_T;  // live pixel windows per row at most kRssT - 1 (plus the demand slot)
+static_assert(kRssT >= 4 && kRssT <= 31, "the worker's pick key holds the slot in 5 bits");
 constexpr uint32_t kRssM24 = 0xFFFFFFu;
 struct RsStream {
     unsigned long long* __restrict__ slots;
@@ -840,6 +845,11 @@ struct RsStream {
     uint32_t jlimit;        // na * 2^14: offsets with an anchor
     int nrows, nchase, nw;  // rows, chaser blocks, live pixel windows per row
     float spread;
+    // live windows and spread follow the live rows (the load law of the
+    // launch-time rule, applied as rows finish): room = room_lanes / live rows;
+    // dyn bit 0: windows, bit 1: spread (an option fixes either)
+    float room_lanes;
+    uint32_t dyn;
     uint32_t watchdog;      // 100-MHz ticks without chain progress before the workers abort
     int test_abort;         // option rowstream_test_abort: chasers leave at once (the abort path's test)
 };
@@ -985,6 +995,8 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
     uint32_t n_wait = 0, n_ext = 0, n_pre = 0, n_sweep = 0;  // statistics (ctl[8..11])
     uint32_t stuck = 0;  // sweeps the chain has waited at the same (x, c)
     float mean = 17.0f;  // draws per sample before any is seen (k_rs_init)
+    float spread = S.spread;
+    uint32_t nw = (uint32_t)S.nw;
     bool done = !mine, err = false;
     unsigned long long* slot = S.slots + (size_t)(mine ? row : 0) * (T + 1u);
     uint32_t* lo = S.lo + (size_t)(mine ? row : 0) * T;
@@ -995,8 +1007,8 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
         const float E = (float)spp * mean * 0.5f, rest = (float)(spp - k) * mean * 0.5f;
         const float i = (float)(q - x);
         const float P = (float)c + rest + (i - 1.0f) * E;
-        const float lo_f = fmaxf((float)c, P - S.spread * sqrtf(i) * E);
-        const float hi_f = P + E + S.spread * sqrtf(i + 1.0f) * E + 2.0f;
+        const float lo_f = fmaxf((float)c, P - spread * sqrtf(i) * E);
+        const float hi_f = P + E + spread * sqrtf(i + 1.0f) * E + 2.0f;
         const uint32_t l = (uint32_t)lo_f, h = min((uint32_t)hi_f, c + cap_span);
         lo[q % T] = l;
         __hip_atomic_exchange(&slot[q % T], rss_win(q, min(l, h), h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1060,12 +1072,22 @@ __device__ void rss_chaser(const RenderArgs& a, const RsStream& S, int wave)
                         done = true;
                         break;
                     }
-                    while (planned + 1u < W && planned < x + (uint32_t)S.nw - 1u) plan(++planned);
+                    if (S.dyn) {  // the rows still chasing set the room per row
+                        const uint32_t live = (uint32_t)S.nrows - min((uint32_t)S.nrows, rss_ld32(&S.ctl[0]));
+                        const float room = S.room_lanes / (float)max(live, 1u);
+                        if (S.dyn & 1u)
+                            nw = (uint32_t)min((int)kRssT - 1, max(2, (int)rintf(2.6f + 1.5f * __logf(fmaxf(room, 1e-3f)))));
+                        if (S.dyn & 2u) spread = fminf(0.25f, fmaxf(0.0f, 0.055f * room - 0.015f));
+                    }
+                    while (planned + 1u < W && planned < x + nw - 1u) plan(++planned);
                 }
             }
             if (moved) __hip_atomic_store(&S.chainpos[row], ((unsigned long long)x << 32) | c, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
             if (done) {
+#ifdef TMPT_EXP_WAVETIME
+                if (row < kWaveTimeMax) g_rowtime[row] = __builtin_amdgcn_s_memrealtime();
+#endif
                 S.rowrays[2 * row] = rays;
                 S.rowrays[2 * row + 1] = erays;
                 if (err) {
@@ -1281,12 +1303,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         const uint32_t hi = (uint32_t)w & kRssM24;
                         const bool valid = ln <= T && p1 > x && p1 <= (uint32_t)a.W && q < hi;
                         // priority: demand, then the lowest pixel; key unique per lane
-                        uint32_t key = valid ? (((ln == T ? 0u : p1 - x) << 4) | ln) : 0xFFFFFFFFu;
+                        uint32_t key = valid ? (((ln == T ? 0u : p1 - x) << 5) | ln) : 0xFFFFFFFFu;
                         // (over all 64 lanes: the pick must be wave-uniform)
                         for (int off = 1; off < 64; off <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, off));
                         if (key != 0xFFFFFFFFu) {
                             moved_on = false;
-                            const int pick = (int)(key & 15u);
+                            const int pick = (int)(key & 31u);
                             uint32_t got = 0, gq = 0, gp = 0;
                             if (ln == (uint32_t)pick) {
                                 const uint32_t n = min((uint32_t)__popcll(nopix), hi - q);
@@ -1316,6 +1338,8 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         crow_rng ^= crow_rng >> 17;
                         crow_rng ^= crow_rng << 5;
                         crow = crow_rng % (uint32_t)S.nrows;
+                        // (taking the laggier of two random rows instead measured within
+                        // noise: profiles/r05_experiments/row_pick2.log)
                     }
                 }
                 if (res >= res_end && (rss_ld32(&S.ctl[0]) >= (uint32_t)S.nrows || rss_ld32(&S.ctl[1]) != 0u))
@@ -3114,6 +3138,12 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     const int64_t lanes = (int64_t)(grid - nchase) * kBlk;
     const double E_est = (double)spp * 8.5;
     const double room = (double)lanes / ((double)rows * E_est);  // resident lanes per pixel window of all rows
+    // Round 5: the chasers re-apply both rules as rows finish (RsStream::dyn,
+    // room per live row): the rows end over ~500 ms of the 1.7 s launch
+    // (profiles/r05_wavetime/row_*.log) and the ones left get more windows;
+    // N=1 1909 -> 1875 ms, 1/2 1085 -> 1054, 1/8 462.5 -> 459.6 (option
+    // rowstream_dynamic; profiles/r05_experiments/row_dynamic_windows.log).
+    // More slots per row (TMPT_RSS_T=16) changed nothing (row_rss16.log).
     int nw = (int)std::lround(2.6 + 1.5 * std::log(std::max(room, 1e-3)));
     nw = std::max(2, std::min(kRssT - 1, nw));
     if (o.rowspec_windows > 0) nw = std::min(kRssT - 1, o.rowspec_windows);
@@ -3219,6 +3249,8 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     // and extension windows are cheaper than a wide spread
     S.spread = o.rowspec_spread >= 0.0f ? o.rowspec_spread
                                         : (float)std::min(0.25, std::max(0.0, 0.055 * room - 0.015));
+    S.room_lanes = (float)((double)lanes / E_est);
+    S.dyn = o.rowstream_dynamic ? ((o.rowspec_windows > 0 ? 0u : 1u) | (o.rowspec_spread >= 0.0f ? 0u : 2u)) : 0u;
     TMPT_HIP(hipMemsetAsync(s.rss_buf, 0, zero_bytes, s.stream));
     {
         const size_t n = (size_t)rows * na;
@@ -3244,6 +3276,32 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     TMPT_HIP(hipGetLastError());
     TMPT_HIP(hipMemcpyAsync(s.rss_host, S.ctl, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     TMPT_HIP(hipStreamSynchronize(s.stream));
+#ifdef TMPT_EXP_WAVETIME
+    {
+        std::vector<unsigned long long> w(3 * kWaveTimeMax, 0ull), r(kWaveTimeMax, 0ull);
+        if (hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wavetime), w.size() * 8) == hipSuccess &&
+            hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rowtime), r.size() * 8) == hipSuccess) {
+            unsigned long long t0 = ~0ull, tend = 0;
+            for (int i = 0; i < kWaveTimeMax; ++i)
+                if (w[3 * i] && w[3 * i + 2]) {
+                    t0 = std::min(t0, w[3 * i]);
+                    tend = std::max(tend, w[3 * i + 2]);
+                }
+            std::vector<double> rt;
+            for (int i = 0; i < std::min(rows, kWaveTimeMax); ++i)
+                if (r[i]) rt.push_back((r[i] - t0) * 0.01);
+            std::sort(rt.begin(), rt.end());
+            auto q = [&](double f) { return rt.empty() ? 0.0 : rt[std::min(rt.size() - 1, (size_t)(f * (rt.size() - 1)))]; };
+            fprintf(stderr, "rowstream rows %zu done at us p0/p10/p50/p90/p99/p100 %.0f/%.0f/%.0f/%.0f/%.0f/%.0f; "
+                            "last worker exit %.0f\n",
+                    rt.size(), q(0), q(0.1), q(0.5), q(0.9), q(0.99), q(1), (tend - t0) * 0.01);
+            std::fill(w.begin(), w.end(), 0ull);
+            std::fill(r.begin(), r.end(), 0ull);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wavetime), w.data(), w.size() * 8);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rowtime), r.data(), r.size() * 8);
+        }
+    }
+#endif
     if (s.rss_host[1] != 0u || s.rss_host[3] != 0u || s.rss_host[0] != (uint32_t)rows) {
 #ifdef TMPT_DIAG
         fprintf(stderr, "rowstream: aborted (rows done %u of %d, abort %u, error %u); iterated engine instead\n",
