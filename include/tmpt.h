@@ -197,7 +197,8 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  * Render options (tmpt_scene_set_option; apply to later renders on the scene):
  *   sample_block     sample seeding: samples per work unit, power of two (0 = auto)
  *   sample_tail      sample seeding: the frame's last sample_tail x (resident lanes) blocks run
- *                    as single-sample units, so the frame ends on one sample, not one block (8)
+ *                    as single-sample units, so the frame ends on one sample, not one block
+ *                    (-1 = auto: a quarter of a lane's samples, at most 64; 0 = off)
  *   sbuf_max         sample seeding: cap in bytes on the per-sample colour
  *                    buffer (0 = 3/4 of free HBM); over the cap a pixel is one unit
  *   sbuf_pair        sample seeding: a unit's samples 2k and 2k+1 written back to back into

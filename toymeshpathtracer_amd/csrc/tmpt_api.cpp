@@ -112,7 +112,7 @@ const OptionDef kOptions[] = {
     {"sah_c_leaf", true, 0, 1e6, nullptr, &Options::sah_c_leaf, nullptr},
     {"sah_c_tri", true, 0, 1e6, nullptr, &Options::sah_c_tri, nullptr},
     {"sample_block", false, 0, 1024, &Options::sample_block, nullptr, nullptr},
-    {"sample_tail", false, 0, 64, &Options::sample_tail, nullptr, nullptr},
+    {"sample_tail", false, -1, 64, &Options::sample_tail, nullptr, nullptr},
     {"sbuf_max", false, 0, 1e18, nullptr, nullptr, &Options::sbuf_max},
     {"sbuf_pair", false, 0, 1, &Options::sbuf_pair, nullptr, nullptr},
     {"pilot", false, -1, 512, &Options::pilot, nullptr, nullptr},

@@ -2745,13 +2745,19 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 #endif
     const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
     // Sample seeding: the work units are (pixel, block of blk samples).  The
-    // block is the largest power of two that still leaves >= kUnitsPerLane
-    // units per resident lane (the frame's tail is then one block of the
-    // heaviest pixel, not its whole sample chain).  Bench frame (1-row bands,
+    // block is the largest power of two up to 8 that still leaves >=
+    // kUnitsPerLane units per resident lane.  Bench frame (1-row bands,
     // k_path ms): N=1 blk 2/4/8 = 220.7/217.8/217.3; 1/2 shard blk 1/2/4/8 =
     // 113.3/110.9/110.2/111.7; 1/4 blk 1/2/4 = 57.1/56.2/56.6; 1/8 blk 1/2/4/8
-    // = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane, so 60 picks 8, 4,
-    // 2, 1 at N = 1, 2, 4, 8.  Option sample_block fixes it.
+    // = 29.4/29.4/30.2/32.7 -- best at ~63 units per lane while the frame
+    // ended on a lane's last block (rounds 2-4: 60 picked 8, 4, 2, 1 at N = 1,
+    // 2, 4, 8).  With the single-sample tail units below the end no longer
+    // depends on the block, and fewer, longer blocks win (round 5, k_path ms,
+    // profiles/r05_experiments/blk_tail_*.log): 1/8 blk 1 / 2 / 4 / 8 with a
+    // 4-block tail 25.55 / 24.93 / 24.54 / 24.73, 1/4 blk 2 / 4 / 8 49.24 /
+    // 48.22 / 48.31, N=1 blk 8 / 16 / 32 186.27 / 186.25 / 188.92, 1/2 blk
+    // 8 / 16 94.47 / 95.09 -- so 15 units per lane and at most 8 samples: 8,
+    // 8, 8, 4 at N = 1, 2, 4, 8.  Option sample_block fixes it.
     uint32_t blk = 1u, nblk = 1u, blk0 = 0u;
     // Progressive passes in sample seeding (samples [s0, s1) of every pixel):
     // the units are the blocks of the pass -- a block size that divides s0, so
@@ -2761,10 +2767,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const bool pass = a.jt && (a.smp_begin > 0 || a.smp_end < a.spp);
     const int64_t s0 = a.smp_begin, s1 = a.smp_end;
     if (a.jt) {
-        constexpr int64_t kUnitsPerLane = 60;
+        constexpr int64_t kUnitsPerLane = 15;
         const int64_t lanes0 = (int64_t)grid * kBlk;
         blk = 1u;
-        while ((int64_t)blk * 2 <= 1024 && blk * 2u <= (uint32_t)(s1 - s0) &&
+        while ((int64_t)blk * 2 <= 8 && blk * 2u <= (uint32_t)(s1 - s0) &&
                a.slots * ((s1 - s0 + blk * 2 - 1) / (blk * 2)) >= kUnitsPerLane * lanes0)
             blk *= 2u;
         if (o.sample_block > 0) blk = (uint32_t)o.sample_block;
@@ -2803,12 +2809,21 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // (profiles/r05_wavetime/; the deferred re-traces are then the last
     // ~2 ms).  k_path, tail 0 / 8 blocks per lane: N=1 188.0 / 186.0 ms, 1/2
     // 96.1 / 94.7 ms (16: slower again, the single units' own seed jumps;
-    // profiles/r05_experiments/sample_tail*.log).
+    // profiles/r05_experiments/sample_tail*.log).  With the longer blocks
+    // above: a quarter of a lane's samples, at most 64 (N=1 and 1/2: 8 blocks
+    // of 8; 1/4: 4 of 8; 1/8: 4 of 4).
     uint32_t ua = 0xFFFFFFFFu;
     // (only when every block is full: a partial last block would map tail
     // units to samples past the pass's end)
-    if (a.jt && nblk > 1 && blk >= 2u && o.sample_tail > 0 && (s1 - s0) % blk == 0) {
-        int64_t nb = std::min<int64_t>(P, (int64_t)o.sample_tail * grid * kBlk);
+    // Auto (-1): a quarter of a lane's samples, at most 64, in blocks.
+    int64_t tail_blocks = o.sample_tail;
+    if (tail_blocks < 0) {
+        const int64_t spl = a.slots * (s1 - s0) / std::max<int64_t>(1, (int64_t)grid * kBlk);  // samples per lane
+        const int64_t b = std::max<uint32_t>(1u, blk);
+        tail_blocks = std::max<int64_t>(1, (std::min<int64_t>(64, spl / 4) + b - 1) / b);
+    }
+    if (a.jt && nblk > 1 && blk >= 2u && tail_blocks > 0 && (s1 - s0) % blk == 0) {
+        int64_t nb = std::min<int64_t>(P, tail_blocks * grid * kBlk);
         while (nb > 0 && (P - nb) + nb * (int64_t)blk >= (1ll << 31)) nb /= 2;
         if (nb > 0) {
             ua = (uint32_t)(P - nb);
