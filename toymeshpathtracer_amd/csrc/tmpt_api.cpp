@@ -407,6 +407,7 @@ int tmpt_scene_destroy(tmpt_scene* h)
     if (s.jt) (void)hipFree(s.jt);
     if (s.sbuf) (void)hipFree(s.sbuf);
     if (s.redo) (void)hipFree(s.redo);
+    if (s.redo_state) (void)hipFree(s.redo_state);
     if (s.jt2) (void)hipFree(s.jt2);
     if (s.rs_buf) (void)hipFree(s.rs_buf);
     for (auto& st : s.rs_stream)

@@ -279,6 +279,7 @@ struct Scene {
     // and the samples the last render left to the redo pass
     uint2* redo = nullptr;
     uint32_t redo_cap = 0;
+    float4* redo_state = nullptr;  // per redo slot: where its path stopped (tmpt_render.hip kRedoState4)
     int64_t redo_samples = 0;
     int64_t redo_late = 0;   // of them, left by the launch's tail to the k_redo launch
     int32_t redo_launches = 0;  // k_redo launches of the last render

@@ -132,9 +132,9 @@ __device__ __forceinline__ int mega_query(const SceneView& sv, f3 o, f3 d, float
 template <bool COUNT, int BLOCK, int SL, bool TOPC = false, bool CHECK_ANY = true>
 __device__ __forceinline__ f3 trace_path(const SceneView& sv, f3 o, f3 d, uint32_t& rng,
                                          uint32_t& rays, uint32_t& srays, TravStack<BLOCK, SL>& st, float* lbuf,
-                                         TravCount& cnt, bool root_check)
+                                         TravCount& cnt, bool root_check, int depth0 = 0)
 {
-    int depth = 0;
+    int depth = depth0;  // > 0: a path resumed at its depth0-th closest-hit query, lbuf[0, depth0) set
     f3 color = mk(0.0f, 0.0f, 0.0f);
     while (depth < kMaxDepth) {  // Trace, main.cpp:89-110
         ++rays;
@@ -277,27 +277,50 @@ __device__ __forceinline__ OctHit octree_walk_wave(const OctNode* __restrict__ n
 }
 
 // ============================================================ deferred ties
-// A sample the deferring sample kernel (k_path DEFER) dropped on a tied
-// closest hit, traced again whole by one lane with ties settled
-// (trace_path's queries end in settle_closest): sample `smp` of tile pixel
-// `pix` from its own seed (sample seeding, main.cpp:212-216), its colour to
-// the colour buffer, where k_resolve_px sums it in sample order.
+// A sample the deferring sample kernel (k_path DEFER) dropped on a flagged
+// closest hit is traced again from that query on by one lane, ties settled
+// (trace_path's queries end in settle_closest).  The drop records where the
+// path stopped -- the query's ray, the RNG state, its depth and the light
+// terms of the bounces before it (redo_state_put) -- so the re-trace resumes
+// there instead of restarting the sample; its colour goes
+// to the colour buffer, where k_resolve_px sums it in sample order.  The list
+// entry is (pixel, sample | depth << 16).
 constexpr uint32_t kRedoEmpty = 0xFFFFFFFFu;  // a list entry not yet written
 constexpr uint32_t kRedoDone = 0xFFFFFFFEu;   // an entry already traced
 constexpr int kRedoTaken = 27, kRedoWaves = 28, kRedoTraced = 29;  // counters[]: tickets, waves past the main loop, traced
+constexpr int kRedoState4 = 5;  // float4 per slot: o.xyz rng, d.xyz -, light[0..9], -, -
+static_assert(2 * 4 + kMaxDepth <= 4 * kRedoState4, "redo state slot too small");
+
+// the state words go out write-through (agent scope: another XCD's lane reads
+// them), before the entry that publishes them (release fence in the caller)
+__device__ __forceinline__ void redo_state_put(float4* ps, f3 o, f3 d, uint32_t rng, const float* light, uint32_t depth,
+                                               uint32_t ls)
+{
+    float* w = reinterpret_cast<float*>(ps);
+    const float h[8] = {o.x, o.y, o.z, __uint_as_float(rng), d.x, d.y, d.z, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 7; ++i) __hip_atomic_store(&w[i], h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = 0; i < depth; ++i)
+        __hip_atomic_store(&w[8 + i], light[i * ls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int BLOCK, int SL>
-__device__ __forceinline__ void redo_sample(const SceneView& sv, const RenderArgs& a, uint32_t pix, uint32_t smp,
-                                            float4* __restrict__ sbuf, uint32_t sb_ss, uint32_t sb_sp,
-                                            uint32_t& rays_e, uint32_t& rays_s, TravStack<BLOCK, SL>& st, float* lbuf)
+__device__ __forceinline__ void redo_sample(const SceneView& sv, const RenderArgs& a, uint32_t pix, uint32_t smp_depth,
+                                            const float4* __restrict__ ps, float4* __restrict__ sbuf, uint32_t sb_ss,
+                                            uint32_t sb_sp, uint32_t& rays_e, uint32_t& rays_s,
+                                            TravStack<BLOCK, SL>& st, float* lbuf)
 {
-    const int lr = (int)(pix / (uint32_t)a.W);
-    const uint32_t x = pix - (uint32_t)lr * (uint32_t)a.W, y = (uint32_t)tile_row_to_y(a, lr);
-    uint32_t rng = sample_seed(a.jt, smp, pixel_seed(x, y, (uint32_t)a.W));
-    f3 o, d;
-    camera_sample(a.cam, x, y, a.invW, a.invH, rng, o, d);
+    const uint32_t smp = smp_depth & 0xFFFFu, depth = smp_depth >> 16;
+    const float* w = reinterpret_cast<const float*>(ps);
+    float h[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) h[i] = __hip_atomic_load(&w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = 0; i < depth; ++i)
+        lbuf[i * BLOCK] = __hip_atomic_load(&w[8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t rng = __float_as_uint(h[3]);
     TravCount cnt;
-    const f3 c = trace_path<false, BLOCK, SL, true, false>(sv, o, d, rng, rays_e, rays_s, st, lbuf, cnt, false);
+    const f3 c = trace_path<false, BLOCK, SL, true, false>(sv, mk(h[0], h[1], h[2]), mk(h[4], h[5], h[6]), rng, rays_e,
+                                                           rays_s, st, lbuf, cnt, false, (int)depth);
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((f32x4){c.x, c.y, c.z, 0.0f},
                                 reinterpret_cast<f32x4*>(sbuf + ((size_t)smp * sb_ss + (size_t)pix * sb_sp)));
@@ -310,10 +333,10 @@ __device__ __forceinline__ uint2 redo_load(const uint2* p)
     return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
 }
 
-__device__ __forceinline__ void redo_put(uint2* p, uint32_t pix, uint32_t smp)
+__device__ __forceinline__ void redo_put(uint2* p, uint32_t pix, uint32_t smp_depth)
 {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)smp << 32) | pix, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)smp_depth << 32) | pix,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void redo_mark(uint2* p)
@@ -325,7 +348,8 @@ __device__ __forceinline__ void redo_mark(uint2* p)
 // see k_path's redo phase): one lane per entry, grid-stride.
 template <int BLOCK, int SL>
 __global__ void __launch_bounds__(BLOCK) k_redo(SceneView sv, RenderArgs a, uint2* __restrict__ list, uint32_t cap,
-                                                float4* __restrict__ sbuf, uint32_t sb_ss, uint32_t sb_sp,
+                                                const float4* __restrict__ state, float4* __restrict__ sbuf,
+                                                uint32_t sb_ss, uint32_t sb_sp,
                                                 uint32_t* __restrict__ ovf, unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_stack[SL * BLOCK];
@@ -344,7 +368,8 @@ __global__ void __launch_bounds__(BLOCK) k_redo(SceneView sv, RenderArgs a, uint
     for (uint32_t i = (uint32_t)gtid; i < n; i += gridDim.x * BLOCK) {
         const uint2 e = list[i];
         if (e.x >= kRedoDone) continue;
-        redo_sample<BLOCK, SL>(sv, a, e.x, e.y, sbuf, sb_ss, sb_sp, rays_e, rays_s, st, &s_light[threadIdx.x]);
+        redo_sample<BLOCK, SL>(sv, a, e.x, e.y, state + (size_t)i * kRedoState4, sbuf, sb_ss, sb_sp, rays_e, rays_s,
+                               st, &s_light[threadIdx.x]);
     }
     const uint32_t re = wave_sum(rays_e), rs = wave_sum(rays_s);
     if (lane_id() == 0 && re + rs) {
@@ -352,6 +377,28 @@ __global__ void __launch_bounds__(BLOCK) k_redo(SceneView sv, RenderArgs a, uint
         atomicAdd(&counters[3], (unsigned long long)re);
         atomicAdd(&counters[kRedoRaysCounter], (unsigned long long)(re + rs));
     }
+}
+
+// the deferred-tie list and its per-slot state (freed together)
+static void free_redo(Scene& s)
+{
+    if (s.redo) (void)hipFree(s.redo);
+    if (s.redo_state) (void)hipFree(s.redo_state);
+    s.redo = nullptr;
+    s.redo_state = nullptr;
+    s.redo_cap = 0;
+}
+static bool alloc_redo(Scene& s, int64_t cap)
+{
+    free_redo(s);
+    if (hipMalloc(&s.redo, sizeof(uint2) * (size_t)cap) != hipSuccess ||
+        hipMalloc(&s.redo_state, sizeof(float4) * kRedoState4 * (size_t)cap) != hipSuccess) {
+        (void)hipGetLastError();
+        free_redo(s);
+        return false;
+    }
+    s.redo_cap = (uint32_t)cap;
+    return true;
 }
 
 template <bool ROW, bool COUNT, int BLOCK, int SL>
@@ -925,6 +972,7 @@ struct PathCtl {
     // main loop trace the listed samples again, ties settled (redo_sample);
     // k_redo takes any they leave.
     uint2* __restrict__ redo;
+    float4* __restrict__ redo_state;  // kRedoState4 float4 per slot: where the dropped path stopped
     uint32_t redo_cap;
     uint32_t redo_inline;  // 0 (test hook, option redo_inline): no redo phase, k_redo takes every entry
     uint32_t redo_lanes;   // lanes per wave that take redo tickets (1..64)
@@ -1502,9 +1550,15 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                                 // could land after that lane's done-mark and undo it
                                 // (k_redo then traced the sample again: rays counted
                                 // twice -- MI355X_MICROARCH.md, per-XCD L2s)
-                                if (slot < (unsigned long long)pc.redo_cap) redo_put(pc.redo + slot, pix, smp);
-                                rays_e -= depth + 1u;
-                                rays_s -= depth;
+                                if (slot < (unsigned long long)pc.redo_cap) {
+                                    redo_state_put(pc.redo_state + (size_t)slot * kRedoState4, r.o, r.d, rng, light,
+                                                   depth, LS);
+                                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // state before entry
+                                    redo_put(pc.redo + slot, pix, smp | (depth << 16));
+                                }
+                                // the re-trace counts this query again and the rest of the
+                                // path; the bounces before it stay counted here
+                                rays_e -= 1u;
                                 depth = 0;
                                 ts.best = -1;
                             }
@@ -1856,7 +1910,9 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
             const bool have = e.x < kRedoDone;
             if (wany(have)) {
                 if (have) {
-                    redo_sample<BLOCK, SL>(sv, a, e.x, e.y, pc.sbuf, pc.sb_ss, pc.sb_sp, rays_e, rays_s, st, light);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the entry before its state
+                    redo_sample<BLOCK, SL>(sv, a, e.x, e.y, pc.redo_state + (size_t)t * kRedoState4, pc.sbuf, pc.sb_ss,
+                                           pc.sb_sp, rays_e, rays_s, st, light);
                     redo_mark(pc.redo + t);
                     atomicAdd(&counters[kRedoTraced], 1ull);
                     t = (uint32_t)atomicAdd(&counters[kRedoTaken], 1ull);
@@ -2946,16 +3002,11 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                            !oct_shadow &&
                            (o.tie_defer > 0 || a.slots * (int64_t)a.spp >= 192 * lanes);
         bool redo = defer && s.oct_view && o.tie_rule == 0;
-        if (redo && o.redo_cap > 0 && s.redo_cap != (uint32_t)o.redo_cap) {  // the test hook's size
-            (void)hipFree(s.redo);
-            s.redo = nullptr;
-            s.redo_cap = 0;
-        }
+        if (redo && o.redo_cap > 0 && s.redo_cap != (uint32_t)o.redo_cap) free_redo(s);  // the test hook's size
         if (redo && s.redo_cap == 0) {
             int64_t cap = std::min<int64_t>(1ll << 31, std::max<int64_t>(1 << 16, a.slots * (int64_t)a.spp / 128));
             if (o.redo_cap > 0) cap = o.redo_cap;
-            if (hipMalloc(&s.redo, sizeof(uint2) * (size_t)cap) == hipSuccess) s.redo_cap = (uint32_t)cap;
-            else (void)hipGetLastError();
+            (void)alloc_redo(s, cap);
         }
         if (redo && s.redo_cap == 0) redo = false;
         // (the deferring kernel keeps the first triangle met on a tie and flags
@@ -2968,6 +3019,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         s.path_launches = 1;
         for (int attempt = 0;; ++attempt) {
             pc.redo = redo ? s.redo : nullptr;
+            pc.redo_state = redo ? s.redo_state : nullptr;
             pc.redo_cap = redo ? s.redo_cap : 0u;
             pc.redo_inline = o.redo_inline ? 1u : 0u;
             pc.redo_lanes = (uint32_t)std::max(1, std::min(64, o.redo_lanes));
@@ -2987,13 +3039,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             if (n > s.redo_cap && attempt == 0) {
                 // the list overflowed: grow it to the count (the same frame lists
                 // the same samples) or, failing that, render with the exact kernel
-                (void)hipFree(s.redo);
-                s.redo = nullptr;
-                s.redo_cap = 0;
-                if (n < (1ull << 31) && hipMalloc(&s.redo, sizeof(uint2) * (size_t)n) == hipSuccess) {
-                    s.redo_cap = (uint32_t)n;
-                } else {
-                    (void)hipGetLastError();
+                if (!(n < (1ull << 31) && alloc_redo(s, (int64_t)n))) {
                     redo = false;
                     fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
                     s.redo_samples = 0;
@@ -3005,8 +3051,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             s.redo_late = (int64_t)(std::min<unsigned long long>(n, s.redo_cap) - std::min(traced, n));
             if (traced < std::min<unsigned long long>(n, s.redo_cap)) {  // entries the launch left
                 TMPT_HIP(hipEventRecord(s.path_ev[0], s.stream));
-                k_redo<kBlk, kPathSL><<<grid, kBlk, 0, s.stream>>>(view(s), as, s.redo, s.redo_cap, pc.sbuf, pc.sb_ss,
-                                                                  pc.sb_sp, (uint32_t*)s.ws, d_counters);
+                k_redo<kBlk, kPathSL><<<grid, kBlk, 0, s.stream>>>(view(s), as, s.redo, s.redo_cap, s.redo_state,
+                                                                  pc.sbuf, pc.sb_ss, pc.sb_sp, (uint32_t*)s.ws,
+                                                                  d_counters);
                 TMPT_HIP(hipGetLastError());
                 TMPT_HIP(hipEventRecord(s.path_ev[1], s.stream));
                 s.redo_launches = 1;  // timed apart from k_path (tmpt_stats.redo_ms)
