@@ -270,7 +270,7 @@ _STREAM = {"rowspec_stream": 1}  # the streaming engine
 
 @pytest.mark.parametrize("opts", [{}, {**_STREAM}, {**_STREAM, "rowspec_windows": 1}, {**_STREAM, "rowspec_spread": 0.0},
                                   {**_STREAM, "rowspec_spread": 0.0, "rowspec_windows": 1},
-                                  {**_STREAM, "rowspec_windows": 7},
+                                  {**_STREAM, "rowspec_windows": 7}, {**_STREAM, "rowstream_dynamic": 0},
                                   {**_ITER}, {**_ITER, "rowspec_wmax": 8}, {**_ITER, "rowspec_wmax": 33},
                                   {**_ITER, "rowspec_windows": 1}, {**_ITER, "rowspec_windows": 1, "rowspec_wmax": 33},
                                   {**_ITER, "rowspec_spread": 0.0}, {**_ITER, "rowspec_spread": 0.0, "rowspec_wmax": 8},
@@ -288,7 +288,8 @@ def test_rowspec_equals_row_chains(gpu, name, w, h, spp, opts):
     units, or placed with no spread, force many iterations per pixel, chains
     that leave a window mid-pixel and next pixels that start before or after
     the lookahead.  Streaming engine: one window ahead or seven, no spread
-    (most pixels then need the chaser's demand or extension windows)."""
+    (most pixels then need the chaser's demand or extension windows), windows
+    fixed at the launch's load or following the rows still chasing."""
     tris, bmin, bmax, sc = _scene(name)
     for k, v in opts.items():
         sc.set_option(k, v)
