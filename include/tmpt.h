@@ -226,6 +226,8 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    also the fallback when the streaming engine does not apply),
  *                    its windows and spread following the rows still chasing
  *                    (1; 0 = fixed at the launch's load)
+ *   row_flag_leaves  row seeding, streaming, with the octree answering ties: the
+ *                    leaves only flag a tie (1; 0 = lowest-index bookkeeping, A/B)
  *   rowstream_test_abort  test hook (0): 1 makes the streaming engine's chaser
  *                    blocks leave at once, so its watchdog (~2 ms then, ~1 s
  *                    normally) aborts the launch and the iterated engine renders

@@ -3175,8 +3175,16 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
 {
     const Options& o = s.opt;
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
-    auto fn2 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
-    auto fn4 = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
+    // with the reference's octree answering (tie_rule visit) the leaves only
+    // flag a tie and keep the first triangle met (TIES 2): the flagged query's
+    // answer comes from the octree either way, so the lowest-index bookkeeping
+    // is not needed (option row_flag_leaves 0 keeps it, for A/B)
+    const bool flag = s.oct_view && o.tie_rule == 0 && o.row_flag_leaves;
+    using RsFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>);
+    const RsFn fn2 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2, false, 2>
+                          : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
+    const RsFn fn4 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4, false, 2>
+                          : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
     const int rows = a.tile_rows;
     const uint32_t W = (uint32_t)a.W, spp = (uint32_t)a.spp, T = (uint32_t)kRssT;
     const size_t lcap = (size_t)a.slots * spp;  // chain samples of the tile
