@@ -228,6 +228,8 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    (1; 0 = fixed at the launch's load)
  *   row_flag_leaves  row seeding, streaming, with the octree answering ties: the
  *                    leaves only flag a tie (1; 0 = lowest-index bookkeeping, A/B)
+ *   row_occ          row seeding, streaming: worker waves per SIMD (0 = by load:
+ *                    5 at full load, 4 with room; or 4, 5)
  *   rowstream_test_abort  test hook (0): 1 makes the streaming engine's chaser
  *                    blocks leave at once, so its watchdog (~2 ms then, ~1 s
  *                    normally) aborts the launch and the iterated engine renders

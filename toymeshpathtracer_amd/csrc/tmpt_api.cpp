@@ -136,6 +136,7 @@ const OptionDef kOptions[] = {
     {"rowspec_stream", false, 0, 1, &Options::rowspec_stream, nullptr, nullptr},
     {"rowstream_dynamic", false, 0, 1, &Options::rowstream_dynamic, nullptr, nullptr},
     {"row_flag_leaves", false, 0, 1, &Options::row_flag_leaves, nullptr, nullptr},
+    {"row_occ", false, 0, 5, &Options::row_occ, nullptr, nullptr},
     {"wf_bins", false, 1, 8, &Options::wf_bins, nullptr, nullptr},
     {"rowstream_test_abort", false, 0, 1, &Options::rowstream_test_abort, nullptr, nullptr},
     {"tie_rule", false, 0, 1, &Options::tie_rule, nullptr, nullptr},

@@ -188,6 +188,7 @@ struct Options {
     int sample_block = 0;     // sample seeding: samples per work unit, a power of two (0 = auto)
     int rowstream_dynamic = 1;  // row seeding, streaming: windows and spread follow the live rows
     int row_flag_leaves = 1;    // row seeding, streaming, octree answering: flag-only leaves (TIES 2)
+    int row_occ = 0;            // row seeding, streaming: worker waves per SIMD (0 = by load, 4, 5)
     int sample_tail = -1;     // sample seeding: blocks per resident lane run as single samples at the end (-1 auto)
     double sbuf_max = 0.0;    // sample seeding: cap on the per-sample colour buffer, bytes (0 = 3/4 of free HBM)
     int sbuf_pair = 1;        // sample seeding: a unit's sample pairs written back to back into one 32-B sector

@@ -2070,7 +2070,10 @@ __global__ void __launch_bounds__(64) k_resolve_px(const float4* __restrict__ sb
 // chain through the window: take the sample at offset 0, add its colour in
 // sample order, jump to offset + its draws, ...  Each window costs ~draws/2
 // traces per chain sample (speculation), but all of them run in parallel.
-constexpr int kRsOcc3 = 5;  // blocks per CU of the shadow-free pass (5 waves per SIMD)
+#ifndef TMPT_RS_OCC
+#define TMPT_RS_OCC 5
+#endif
+constexpr int kRsOcc3 = TMPT_RS_OCC;  // blocks per CU of the shadow-free pass (5 waves per SIMD)
 constexpr int kRsMaxWin = 32;  // windows per row and iteration: this pixel + up to 31 lookaheads
 
 struct RowSpec {
@@ -3183,8 +3186,11 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     using RsFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>);
     const RsFn fn2 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2, false, 2>
                           : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
-    const RsFn fn4 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4, false, 2>
-                          : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
+    RsFn fn4 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4, false, 2>
+                    : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
+    // the workers at 4 waves per SIMD (no spills) for light loads (option row_occ)
+    const RsFn fn4_occ4 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 4, false, 2>
+                               : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 4>;
     const int rows = a.tile_rows;
     const uint32_t W = (uint32_t)a.W, spp = (uint32_t)a.spp, T = (uint32_t)kRssT;
     const size_t lcap = (size_t)a.slots * spp;  // chain samples of the tile
@@ -3196,10 +3202,25 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     // plus 2^20 of room for the workers' fetch-adds past a window's end
     if (rows < 1 || W > 4094u || (uint64_t)W * spp * 14u + R + (1u << 20) >= (1ull << 24) || lcap >= (1ull << 31))
         return 1;
-    const int grid = occupancy_grid((const void*)fn4, kBlk, 0, s.device);
+    int grid = occupancy_grid((const void*)fn4, kBlk, 0, s.device);
     const int grid2 = occupancy_grid((const void*)fn2, kBlk, 0, s.device);
     const int nchase = (rows + kBlk - 1) / kBlk;  // blocks of 4 waves x 64 rows
     if (grid <= 2 * nchase) return 1;
+    {
+        // 5 waves per SIMD (96 VGPRs, 10 spilled dwords) win at full load, 4
+        // (no spills) once the GPU has room per row: bench frame, row seeding,
+        // 4 / 5 / 6 waves, N=1 1944.7 / 1854.6 / 1889.9 ms, 1/8 436.0 / 450.5 /
+        // 477.1 ms; 4 / 5 waves at 1/2 1048.8 / 1043.6, 1/4 639.7 / 658.9, 1/8
+        // 434.4 / 450.4 ms (room 1.1, 2.2, 4.4; profiles/r05_experiments/
+        // row_worker_occupancy*.log): 4 waves from room 1.6
+        const double room5 = (double)(grid - nchase) * kBlk / ((double)rows * (double)spp * 8.5);
+        const bool occ4 = o.row_occ == 4 || (o.row_occ == 0 && room5 >= 1.6);
+        const int g4 = occ4 ? occupancy_grid((const void*)fn4_occ4, kBlk, 0, s.device) : 0;
+        if (occ4 && g4 > 2 * nchase) {
+            fn4 = fn4_occ4;
+            grid = g4;
+        }
+    }
     // live windows per row: 2.6 + 1.5 ln(room), room = resident lanes per
     // pixel window of all rows, within 2..kRssT-1.  Bench frame, 64 spp
     // (profiles/r03_rowspec/stream_windows_*, with the spread rule below):
