@@ -197,6 +197,7 @@ __device__ unsigned long long g_crackstat[4];
 constexpr int kWaveTimeMax = 16384;
 __device__ unsigned long long g_wavetime[3 * kWaveTimeMax];
 __device__ unsigned long long g_rowtime[kWaveTimeMax];  // streaming row engine: when each row's chain ended
+__device__ unsigned long long g_claimtime[kWaveTimeMax];  // streaming row engine: each worker wave's last claim
 #endif
 
 // ============================================================ octree walk, one wave
@@ -1373,6 +1374,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                             if (!got) ++n_cas;
                             if (got) {
                                 ++n_claim;
+#ifdef TMPT_EXP_WAVETIME  // the row workers: when each wave last found speculation work
+                                if (lane_id() == 0 && wt_id < kWaveTimeMax)
+                                    g_claimtime[wt_id] = __builtin_amdgcn_s_memrealtime();
+#endif
                                 res = (uint32_t)__shfl((int)gq, pick);
                                 res_end = res + got;
                                 srow = crow;
@@ -3369,9 +3374,10 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     TMPT_HIP(hipStreamSynchronize(s.stream));
 #ifdef TMPT_EXP_WAVETIME
     {
-        std::vector<unsigned long long> w(3 * kWaveTimeMax, 0ull), r(kWaveTimeMax, 0ull);
+        std::vector<unsigned long long> w(3 * kWaveTimeMax, 0ull), r(kWaveTimeMax, 0ull), cl(kWaveTimeMax, 0ull);
         if (hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wavetime), w.size() * 8) == hipSuccess &&
-            hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rowtime), r.size() * 8) == hipSuccess) {
+            hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rowtime), r.size() * 8) == hipSuccess &&
+            hipMemcpyFromSymbol(cl.data(), HIP_SYMBOL(g_claimtime), cl.size() * 8) == hipSuccess) {
             unsigned long long t0 = ~0ull, tend = 0;
             for (int i = 0; i < kWaveTimeMax; ++i)
                 if (w[3 * i] && w[3 * i + 2]) {
@@ -3386,10 +3392,19 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
             fprintf(stderr, "rowstream rows %zu done at us p0/p10/p50/p90/p99/p100 %.0f/%.0f/%.0f/%.0f/%.0f/%.0f; "
                             "last worker exit %.0f\n",
                     rt.size(), q(0), q(0.1), q(0.5), q(0.9), q(0.99), q(1), (tend - t0) * 0.01);
+            std::vector<double> lc;  // each worker wave's last claim of speculation work
+            for (int i = 0; i < kWaveTimeMax; ++i)
+                if (w[3 * i] && w[3 * i + 2] && cl[i]) lc.push_back((cl[i] - t0) * 0.01);
+            std::sort(lc.begin(), lc.end());
+            auto ql = [&](double f) { return lc.empty() ? 0.0 : lc[std::min(lc.size() - 1, (size_t)(f * (lc.size() - 1)))]; };
+            fprintf(stderr, "rowstream workers %zu: last claim at us p0/p10/p25/p50/p75/p90/p100 "
+                            "%.0f/%.0f/%.0f/%.0f/%.0f/%.0f/%.0f\n",
+                    lc.size(), ql(0), ql(0.1), ql(0.25), ql(0.5), ql(0.75), ql(0.9), ql(1));
             std::fill(w.begin(), w.end(), 0ull);
             std::fill(r.begin(), r.end(), 0ull);
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wavetime), w.data(), w.size() * 8);
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rowtime), r.data(), r.size() * 8);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_claimtime), r.data(), r.size() * 8);
         }
     }
 #endif
