@@ -280,8 +280,9 @@ def host_cpus() -> dict:
 
 def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
     """The CPU restatement of the reference algorithm (octree + Moller-Trumbore,
-    oracle/) on ALL host cores -- as many threads as the process may use, like
-    TBB's default_num_threads() (main.cpp:250-251) -- timed on a bounded sample
+    oracle/) on every CPU the process may use -- like TBB's default_num_threads()
+    (main.cpp:250-251), but counted as the cgroup quota grants them, not as the
+    host's thread count -- timed on a bounded sample
     of the same frame: batches of rows y = o (mod S), S ~ H / (2 threads) (two rows per
     thread), of which the pixels x = c (mod 32) (pixel and sample seeding:
     pixels are independent; row seeding renders whole rows of fewer rows per
@@ -290,7 +291,11 @@ def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
     GPU frame (octree tie order)."""
     import oracle
     hc = host_cpus()
-    threads = max(1, min(hc["nproc"], 256))  # the oracle's thread pool holds at most 256
+    # the CPUs the process may actually use: its affinity, capped by the
+    # cgroup's CPU quota (the GPU box grants 16 of 256 host threads; more
+    # threads than that only oversubscribe the quota); the oracle's pool holds <= 256
+    eff = hc["nproc"] if not hc["cgroup_cpu_quota"] else min(hc["nproc"], max(1, int(hc["cgroup_cpu_quota"])))
+    threads = max(1, min(eff, 256))
     osc = oracle.Scene(tris, accel=oracle.ACCEL_OCTREE, tie=oracle.TIE_VISIT, bmin=bmin, bmax=bmax)
     seed = {"sample": oracle.SEED_SAMPLE, "pixel": oracle.SEED_PIXEL, "row": oracle.SEED_ROW}[args.seed_mode]
     row_mode = args.seed_mode == "row"
@@ -316,12 +321,31 @@ def cpu_baseline(args, tris, bmin, bmax, cam, W, H, SPP, frame):
     cpu = {"value": round(crays / cdt / 1e6, 3), "unit": "MRays/s", "cores": threads, "kind": "port",
            "threads": threads, **hc,
            "sample": f"{npx} of {W * H} px ({nb} batches of rows y%{stride}==o, pixels x%{xs}==c) x {SPP} spp, "
-                     f"{crays} rays, {cdt:.1f} s on {threads} threads (the box grants "
-                     f"{hc['cgroup_cpu_quota'] or hc['nproc']} CPUs); octree restatement of scene.cpp, "
+                     f"{crays} rays, {cdt:.1f} s on {threads} threads = the effective CPUs (affinity "
+                     f"{hc['nproc']}, cgroup quota {hc['cgroup_cpu_quota']}); octree restatement of scene.cpp, "
                      f"{args.seed_mode} seeding"}
     diff = int(((frame != ref).any(-1) & mask).sum())
     parity = {"pixels_checked": npx, "pixels_differ": diff, "oracle": "octree (reference tie order)"}
     return cpu, parity
+
+
+def device_identity(local: int) -> dict:
+    """The physical device this rank opened: PCI domain:bus:device and UUID
+    (hipDeviceProp_t via torch), so an N>1 line proves which GPUs it ran on."""
+    p = torch.cuda.get_device_properties(local)
+    return {"pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid),
+            "name": p.name, "local_rank": local}
+
+
+def world_devices(ident: dict, world: int, dist_on: bool, backend: str) -> dict:
+    """Every rank's device identity gathered to all ranks, summarised by
+    shard.placement (`n_gpus` = distinct devices; a gloo rehearsal whose ranks
+    share one GPU reports 1 with `ranks` N and `rehearsal` true)."""
+    devs = [ident]
+    if dist_on:
+        devs = [None] * world
+        dist.all_gather_object(devs, ident)
+    return sharding.placement(devs, backend if dist_on else None)
 
 
 @contextlib.contextmanager
@@ -367,6 +391,7 @@ def main() -> None:
             else:
                 dist.init_process_group("gloo")
             dist.barrier()
+    placement = world_devices(device_identity(local), world, dist_on, args.dist_backend)
 
     obj, W, H, SPP, sponza = CONFIGS[args.config]
     path = scene_path(obj)
@@ -420,6 +445,7 @@ def main() -> None:
     ties = roots = redo = redo_late = cracks = 0
     redo_launches = redo_rays = 0
     redo_ms = 0.0
+    last_tie_path = 0
     for _ in range(args.steps):
         r, st = step()
         ties += st.tie_queries
@@ -430,6 +456,7 @@ def main() -> None:
         redo_launches += st.redo_launches
         redo_ms += st.redo_ms
         redo_rays += st.redo_rays
+        last_tie_path = st.tie_path
         rays += r
         ext_ms += st.extend_ms
         sh_ms += st.shadow_ms
@@ -607,7 +634,9 @@ def main() -> None:
         os.remove(png)
 
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "MRays/s", "n_gpus": world,
+        "metric": METRIC, "value": round(value, 2), "unit": "MRays/s", "n_gpus": placement["n_gpus"],
+        "ranks": placement["ranks"], "dist_backend": placement["dist_backend"], "devices": placement["devices"],
+        "rehearsal": placement["rehearsal"],
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
@@ -637,6 +666,12 @@ def main() -> None:
                              # sample seeding at >= 192 samples per lane: tied samples dropped by
                              # the main loop and traced again in the launch's tail
                              "tie_answer": "deferred" if redo else "in the main loop",
+                             # tmpt_stats.tie_path of the last timed render: 1 main loop, 2 deferred,
+                             # 3 deferral chosen but its list did not fit (main loop)
+                             "tie_path": last_tie_path,
+                             # triangles flat on an octree plane: with any, shadow answers are
+                             # checked too and the deferral / shadow offload are off
+                             "octree_flat": st0.octree_flat,
                              "redo_samples_per_step": redo // max(args.steps, 1),
                              "redo_late_total": redo_late,
                              "index_rule": index_rule},

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMPT_ABI_VERSION 8  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
+#define TMPT_ABI_VERSION 9  /* 2: progressive spp (spp_begin / spp_count); 3: tmpt_render_multi;
                               4: tmpt_unit_sincos; 5: wait_stream (TMPT_FLAG_WAIT_STREAM),
                               progressive continuation keyed on the camera,
                               TMPT_SEED_SAMPLE; 6: scene options (tmpt_scene_create_ex,
@@ -38,7 +38,9 @@ extern "C" {
                               options tie_defer / redo_cap, tmpt_stats.redo_samples;
                               8: the octree answers crack queries and flat triangles too
                               (tmpt_stats.crack_queries, octree_flat), tmpt_stats.redo_launches /
-                              redo_ms (k_redo apart from the k_path launches) */
+                              redo_ms (k_redo apart from the k_path launches);
+                              9: tmpt_stats.tie_path (how the last render answered the
+                              octree's queries, and whether the deferred form fell back) */
 
 typedef struct tmpt_scene tmpt_scene; /* opaque, device-resident */
 
@@ -147,6 +149,12 @@ typedef struct {
     int32_t redo_launches;    /* sample seeding, tie_defer: k_redo launches of the last render (0 or 1) */
     double redo_ms;           /* their time; extend_ms holds the main k_path launches only */
     uint64_t redo_rays;       /* their queries (part of the render's ray count) */
+    /* (ABI 9) how the last render answered the queries the octree decides: 0 none (no octree,
+     * tie_rule = index, or not a k_path render), 1 in the main loop (the wave's octree walk or
+     * the serial walk), 2 deferred (tie_defer: dropped samples traced again in the launch's
+     * tail), 3 deferral chosen but its list could not be allocated: answered in the main loop */
+    int32_t tie_path;
+    int32_t reserved_stats;
 } tmpt_stats;
 
 /* ---- host side: scene ingest and camera (not kernels) ------------------- */

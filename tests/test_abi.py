@@ -47,7 +47,7 @@ def test_no_oracle_or_torch_in_the_product_library():
 
 
 def test_abi_version_and_error_channel():
-    assert tm.abi_version() == 8
+    assert tm.abi_version() == 9
     with pytest.raises(tm.TmptError) as e:
         tm.load_scene("/definitely/missing.obj")
     assert "missing.obj" in str(e.value)
@@ -113,10 +113,10 @@ def test_scene_options_are_checked_before_any_device_work():
     tris = np.zeros((1, 9), np.float32)
     for bad, msg in (("bogus=1", "unknown option"), ("leaf_max=0", "out of range"), ("leaf_max=x", "bad value"),
                      ("builder=kd", "bad value"), ("sample_block=3", "power of two"), ("leaf_max", "no value"),
-                     ("pilot=1.5", "integer")):
+                     ("pilot=1.5", "integer"), ("row_occ=2", "0 \\(by load\\), 4 or 5")):
         with pytest.raises(tm.TmptError, match=msg):
             tm.Scene(tris, options=bad)
     if tm.device_count() == 0:
-        for good in ("builder=lbvh, leaf_max=4", {"collapse": "sah", "ploc_radius": 8}, "", None):
+        for good in ("builder=lbvh, leaf_max=4", {"collapse": "sah", "ploc_radius": 8}, "", None, "row_occ=4"):
             with pytest.raises(tm.TmptError, match="device"):
                 tm.Scene(tris, options=good)

@@ -83,3 +83,42 @@ def test_bench_refuses_a_mislabelled_gpu_count():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "1"], cwd=root, capture_output=True, text=True,
                        timeout=300, env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
     assert r.returncode == 2 and "WORLD_SIZE 2" in r.stderr and not r.stdout.strip()
+
+
+def _placement_worker(rank, world, port, out_path):
+    """bench.py's device census over gloo: each rank contributes its device
+    identity (here fake: ranks 0 and 1 share a device, as in the one-GPU
+    rehearsal), rank 0 summarises with shard.placement."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from toymeshpathtracer_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ident = {"pci": f"0000:{0x10 + max(rank - 1, 0):02x}:00", "uuid": f"gpu{max(rank - 1, 0)}"}
+    devs = [None] * world
+    dist.all_gather_object(devs, ident)
+    if rank == 0:
+        import json
+        with open(out_path, "w") as f:
+            json.dump(shard.placement(devs, "gloo"), f)
+    dist.destroy_process_group()
+
+
+def test_placement_counts_distinct_devices(tmp_path):
+    """The N>1 bench line's n_gpus is the number of DISTINCT devices the ranks
+    opened: 3 gloo ranks on 2 devices say n_gpus 2,
+    ranks 3, rehearsal true; one rank per device says rehearsal false."""
+    import json
+    from toymeshpathtracer_amd import shard
+    out = str(tmp_path / "placement.json")
+    mp.spawn(_placement_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    with open(out) as f:
+        p = json.load(f)
+    assert p == {"n_gpus": 2, "ranks": 3, "dist_backend": "gloo",
+                 "devices": ["0000:10:00", "0000:10:00", "0000:11:00"], "rehearsal": True}
+    own = shard.placement([{"pci": f"0000:{i:02x}:00", "uuid": str(i)} for i in range(8)], "nccl")
+    assert own["n_gpus"] == 8 and own["ranks"] == 8 and own["rehearsal"] is False
+    assert shard.placement([{"pci": "0000:05:00", "uuid": "a"}], None)["dist_backend"] is None

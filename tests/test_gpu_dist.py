@@ -35,16 +35,20 @@ def _bench(args, env_extra=None, timeout=600):
     return json.loads(lines[0])
 
 
-def test_bench_two_ranks_gloo_matches_single(gpu, tmp_path):
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_ranks_gloo_matches_single(gpu, tmp_path, ranks):
     one = tmp_path / "one.png"
     two = tmp_path / "two.png"
     common = ["--config", "teapot720", "--steps", "1", "--warmup", "0", "--no-cpu"]
     r1 = _bench(["bench.py", "--gpus", "1", "--save", str(one)] + common)
     port = _free_port()
-    r2 = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                 "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+    r2 = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+                 "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(ranks),
                  "--dist-backend", "gloo", "--save", str(two)] + common)
-    assert r2["n_gpus"] == 2 and r2["scaling"] == "strong"
+    # ranks sharing the box's one GPU: a rehearsal, one distinct device
+    assert r2["n_gpus"] == 1 and r2["ranks"] == ranks and r2["rehearsal"] is True and r2["scaling"] == "strong"
+    assert r2["dist_backend"] == "gloo" and len(r2["devices"]) == ranks and len(set(r2["devices"])) == 1
+    assert r1["n_gpus"] == 1 and r1["ranks"] == 1 and r1["rehearsal"] is False and r1["dist_backend"] is None
     assert r2["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
     a = np.asarray(Image.open(one).convert("RGBA"))
     b = np.asarray(Image.open(two).convert("RGBA"))
@@ -65,6 +69,9 @@ def test_bench_rccl_path_one_rank(gpu, tmp_path):
     r2 = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
                  "--master-port", str(port), "bench.py", "--gpus", "1", "--force-dist", "--save", str(rccl)] + common)
     assert r2["n_gpus"] == 1 and r2["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
+    # the RCCL line names its backend and the one device's PCI address
+    assert r2["dist_backend"] == "nccl" and r2["ranks"] == 1 and r2["rehearsal"] is False
+    assert len(r2["devices"]) == 1 and r2["devices"] == r1["devices"] and ":" in r2["devices"][0]
     a = np.asarray(Image.open(one).convert("RGBA"))
     b = np.asarray(Image.open(rccl).convert("RGBA"))
     assert np.array_equal(a, b)
@@ -73,7 +80,8 @@ def test_bench_rccl_path_one_rank(gpu, tmp_path):
 def test_bench_gpus_n_launches_its_own_ranks(gpu, tmp_path):
     """`python bench.py --gpus 2` with no launcher around it starts its two
     ranks itself (torch.distributed.run as a child, before any GPU call): with
-    the gloo rehearsal both share the box's GPU and the line says n_gpus 2;
+    the gloo rehearsal both share the box's GPU and the line says ranks 2 on
+    n_gpus 1 (one distinct device, rehearsal true);
     with nccl (one rank per GPU) on a box with fewer GPUs it exits non-zero
     and says why, instead of measuring one GPU."""
     import toymeshpathtracer_amd as tm
@@ -88,7 +96,8 @@ def test_bench_gpus_n_launches_its_own_ranks(gpu, tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
+    assert line["n_gpus"] == 1 and line["ranks"] == 2 and line["rehearsal"] is True
+    assert line["config"]["rays_per_step"] == r1["config"]["rays_per_step"]
     assert np.array_equal(np.asarray(Image.open(one)), np.asarray(Image.open(two)))
     if tm.device_count() < 2:
         r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + common, cwd=ROOT, capture_output=True,

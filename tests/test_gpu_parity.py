@@ -661,6 +661,24 @@ def test_progressive_shards_and_errors(gpu):
     sc.close()
 
 
+def test_progressive_sample_pass_unit_bound(gpu):
+    """a sample-seeding pass whose first sample forces small
+    blocks can need more than 2^31 sample units (unit ids are 32-bit); it is
+    refused with an error, not wrapped.  4096 x 4096 x 258 spp from sample 2:
+    blocks of 2, 16.8 M pixels x 128 blocks = 2.15 G units (the colour buffer,
+    69 GB, fits the device, so the call reaches the bound)."""
+    tris, bmin, bmax, sc = _scene("cube.obj")
+    w = h = 4096
+    spp = 258
+    cam = tm.Camera.for_scene(bmin, bmax, w, h)
+    sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, spp_begin=0, spp_count=2)
+    with pytest.raises(tm.TmptError, match="2\\^31"):
+        sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, spp_begin=2, spp_count=spp - 2)
+    # a fresh first pass of the same frame still renders
+    sc.trace_image(cam, w, h, spp, seed_mode=tm.SEED_SAMPLE, spp_begin=0, spp_count=2)
+    sc.close()
+
+
 # ---------------------------------------------------------------- edge cases
 def _oracle_pixel(tris, cam, w, h, spp):
     osc = oracle.Scene(tris, accel=oracle.ACCEL_LINEAR if len(tris) < 64 else oracle.ACCEL_BVH,

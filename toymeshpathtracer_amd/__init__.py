@@ -109,7 +109,7 @@ class _Stats(ctypes.Structure):
                 ("redo_samples", ctypes.c_int64), ("redo_late", ctypes.c_int64),
                 ("crack_queries", ctypes.c_uint64), ("octree_flat", ctypes.c_int32),
                 ("redo_launches", ctypes.c_int32), ("redo_ms", ctypes.c_double),
-                ("redo_rays", ctypes.c_uint64)]
+                ("redo_rays", ctypes.c_uint64), ("tie_path", ctypes.c_int32), ("reserved_stats", ctypes.c_int32)]
 
 
 def _sig(name, res, args):
@@ -350,6 +350,7 @@ class RenderStats:
     redo_launches: int
     redo_ms: float
     redo_rays: int
+    tie_path: int
 
 
 def _desc(width, height, spp, seed_mode, band_rows=0, shard=0, num_shards=1,

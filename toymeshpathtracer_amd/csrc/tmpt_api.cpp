@@ -171,6 +171,10 @@ int options_set(Options& o, const char* key, double v, bool allow_build)
             set_error(std::string("option '") + key + "' takes an integer");
             return -22;
         }
+        if (strcmp(key, "row_occ") == 0 && v != 0 && v != 4 && v != 5) {  // waves per SIMD: by load, 4 or 5
+            set_error("option 'row_occ' takes 0 (by load), 4 or 5");
+            return -22;
+        }
         if ((strcmp(key, "sample_block") == 0 || strcmp(key, "wf_bins") == 0) && v > 0 &&
             ((long long)v & ((long long)v - 1)) != 0) {
             set_error(std::string("option '") + key + "' must be a power of two");
@@ -486,6 +490,11 @@ int tmpt_scene_build_octree(tmpt_scene* h, const float bmin[3], const float bmax
     if (hipMemcpy(s.oct_view, &ov, sizeof(ov), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d_nodes);
         (void)hipFree(d_refs);
+        // the previous octree (if any) stays in use: give the records back its
+        // own flat marks (none without one), so marks and octree agree
+        std::vector<uint8_t> old_flat((size_t)s.n, 0);
+        if (s.oct) (void)octree_flat_triangles(s.tris_host.data(), s.n, s.oct_grid, old_flat);
+        (void)mark_flat_triangles(s, old_flat);
         return (set_error("tmpt_scene_build_octree: upload failed"), -1);
     }
     if (s.oct) (void)hipFree(s.oct);
@@ -910,6 +919,8 @@ int tmpt_get_stats(const tmpt_scene* h, tmpt_stats* o)
     o->redo_launches = s.redo_launches;
     o->redo_ms = s.redo_ms;
     o->redo_rays = s.redo_rays;
+    o->tie_path = s.tie_path;
+    o->reserved_stats = 0;
     return 0;
 }
 

@@ -285,6 +285,7 @@ struct Scene {
     int64_t redo_samples = 0;
     int64_t redo_late = 0;   // of them, left by the launch's tail to the k_redo launch
     int32_t redo_launches = 0;  // k_redo launches of the last render
+    int32_t tie_path = 0;       // tmpt_stats.tie_path of the last render
     double redo_ms = 0.0;       // and their time (not in extend_ms)
     uint64_t redo_rays = 0;     // and their rays (in the render's count)
     // speculative row seeding (tmpt_render.hip render_rowspec): jump tables

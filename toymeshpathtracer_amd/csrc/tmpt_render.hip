@@ -1534,9 +1534,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     // the triangle index (2 x index | tie flag in the leaves'
                     // records); a tie was answered over the octree at the top of
                     // the round, or (DEFER) drops the sample here
-#ifdef TMPT_EXP_NOSETTLE  // cost experiment: no octree re-answer
-                    ts.best >>= 1;
-#else
                     bool drop = false;
                     if (DEFER) {
                         // the deferring kernel: a tied sample is dropped here
@@ -1578,7 +1575,6 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     } else if (!settled) {
                         ts.best >>= 1;  // the index (a tie was answered above)
                     }
-#endif
                     if (ts.best >= 0) {  // Scatter, main.cpp:44-73
                         // the hit record's loads go out first; RandomUnitVector
                         // (RNG + sincos, independent of them) runs while they are
@@ -1711,11 +1707,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         // the unit is held in `col` (unused with a colour buffer) and
                         // written with it, back to back into one 32-B sector
                         const bool odd = (smp & 1u) != 0u;
-#ifdef TMPT_EXP_NOPAIR  // cost experiment: no paired stores
-                        if (false) {
-#else
                         if (pc.pair && !odd && !single && smp + 1u < (uint32_t)a.smp_end && ((smp + 1u) & a.bmask) != 0u) {
-#endif
                             col = color;
                         } else {
                             // DEFER: a dropped sample's slot (x = -1) is redo_sample's
@@ -1780,12 +1772,10 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                 qany = sany;
                 if (sany) ++rays_s; else ++rays_e;
                 in_query = sv.n > 0 && !ray_has_nan(so, sd);  // NaN ray / no triangles: a counted miss
-#ifndef TMPT_EXP_NOROOT  // cost experiment: no root box test
                 if (!DEFER && a.root_check && cam && in_query && !octree_root_hit(sv, so, sd, kMinT, kMaxT)) {
                     in_query = false;  // a camera ray outside the reference's root box: a counted miss
                     atomicAdd(&sv.oct->ties[1], 1ull);
                 }
-#endif
             }
             if (PROF >= 2) ps_start += stamp() - ps_t;
         }
@@ -2840,6 +2830,17 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         if (o.sample_block > 0) blk = (uint32_t)o.sample_block;
         while (a.slots * ((s1 - s0 + blk - 1) / blk) >= (1ll << 31)) blk *= 2u;  // 32-bit unit ids
         while (s0 % blk) blk /= 2u;  // a pass's first sample starts a block
+        // the alignment can undo the 32-bit guard above (e.g. 4K x 1024 spp
+        // from spp_begin 2: blocks of 2, ~4.2 G units): the unit ids, res and
+        // nchunks are uint32, so such a pass is refused, not wrapped
+        if (a.slots * ((s1 - s0 + blk - 1) / blk) >= (1ll << 31)) {
+            set_error("tmpt_render: this progressive pass (samples " + std::to_string(s0) + ".." +
+                      std::to_string(s1) + " of " + std::to_string(a.slots) +
+                      " pixels) needs more than 2^31 sample units at the block size its first sample allows (" +
+                      std::to_string(blk) + "): start passes at a multiple of a larger power of two, or render "
+                      "the frame in one call");
+            return -22;
+        }
         blk0 = (uint32_t)(s0 / blk);
         nblk = (uint32_t)((s1 + blk - 1) / blk - blk0);
         // Several blocks per pixel need the per-sample colour buffer (16 B per
@@ -3016,7 +3017,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             if (o.redo_cap > 0) cap = o.redo_cap;
             (void)alloc_redo(s, cap);
         }
-        if (redo && s.redo_cap == 0) redo = false;
+        const bool redo_nomem = redo && s.redo_cap == 0;
+        if (redo_nomem) redo = false;
         // (the deferring kernel keeps the first triangle met on a tie and flags
         // it: only the redo pass gives those samples their answer)
         // (with the octree but no deferral: the leaf only flags ties, TIES 2)
@@ -3024,6 +3026,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
         else if (fn == fn_default && a.jt && !count && !soa && s.oct_view && o.tie_rule == 0)
             fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
+        s.tie_path = !(s.oct_view && o.tie_rule == 0) ? 0 : redo ? 2 : redo_nomem ? 3 : 1;
         s.path_launches = 1;
         for (int attempt = 0;; ++attempt) {
             pc.redo = redo ? s.redo : nullptr;
@@ -3051,6 +3054,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                     redo = false;
                     fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
                     s.redo_samples = 0;
+                    s.tie_path = 3;
                 }
                 TMPT_HIP(hipMemsetAsync(d_counters, 0, kRenderCounters * sizeof(unsigned long long), s.stream));
                 TMPT_HIP(hipMemsetAsync(heads, 0, head_words * 4, s.stream));
@@ -3075,6 +3079,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         }
         return 0;
     }
+    s.tie_path = s.oct_view && o.tie_rule == 0 ? 1 : 0;  // pixel seeding answers in the main loop
     uint32_t* base = heads + head_words;
     float4* state = reinterpret_cast<float4*>(base);  // P x {colour sum, rng}
     uint32_t* cost = base + 4 * (size_t)P;
@@ -3972,6 +3977,7 @@ int render(Scene& s, const tmpt_camera* cam, const tmpt_render_desc* d, uint32_t
     s.redo_launches = 0;
     s.redo_ms = 0.0;
     s.redo_rays = 0;
+    s.tie_path = 0;
     if (a.slots > 0) {
         if (wave) rc = render_wavefront(s, a, d_out, count);
         else if (persistent) rc = render_persistent(s, a, d_out, count, d_counters);

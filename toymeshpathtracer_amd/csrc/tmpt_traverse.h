@@ -365,21 +365,6 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
                                           mk(b1.z, b1.w, c1.x), tmin, tmax, t1, u1, w1) &&
                              n > 1u;
             const int id0 = __float_as_int(c0.y), id1 = __float_as_int(c1.y);
-#ifdef TMPT_EXP_NOTIE  // cost experiment: no tie flag (wrong answers on ties)
-            const bool tie0 = false, tie1 = false;
-            const bool acc0 = ok0 && (t0 < ts.bt || (t0 == ts.bt && ts.best >= 0 && id0 < ts.best));
-            ts.bt = acc0 ? t0 : ts.bt;
-            ts.bu = acc0 ? u0 : ts.bu;
-            ts.bv = acc0 ? w0 : ts.bv;
-            ts.best = acc0 ? id0 : ts.best;
-            const bool acc1 = ok1 && !(any && acc0) && (t1 < ts.bt || (t1 == ts.bt && ts.best >= 0 && id1 < ts.best));
-            ts.bt = acc1 ? t1 : ts.bt;
-            ts.bu = acc1 ? u1 : ts.bu;
-            ts.bv = acc1 ? w1 : ts.bv;
-            ts.best = acc1 ? id1 : ts.best;
-            (void)tie0;
-            (void)tie1;
-#else
             // FLAG: the first triangle met keeps a tie (the flag sends the query
             // to be answered again); otherwise the lower index takes it
             const bool tie0 = ok0 && t0 == ts.bt;
@@ -394,7 +379,6 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             ts.bu = acc1 ? u1 : ts.bu;
             ts.bv = acc1 ? w1 : ts.bv;
             ts.best = (acc1 ? id1 : ts.best) | (int)tie1;
-#endif
             if (any && (acc0 || acc1)) return true;
         } else {  // a lone lane (row chains) gains more from the early exits
             if (tri(a0, b0, c0)) return true;
@@ -584,9 +568,6 @@ __device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& 
 {
     if (sv.oct == nullptr || ts.best < 0) return false;
     if ((ts.best & 1) != 0) return true;
-#ifdef TMPT_EXP_NOCRACK  // cost experiment: no crack test (wrong answers on crack queries)
-    return false;
-#else
     // first stage from the by-value copy (no memory round trip); the plane
     // distances, rarely needed, through the view
     const float span = fminf(ts.bt, sv.crack.x);
@@ -604,7 +585,6 @@ __device__ __forceinline__ bool octree_flag(const SceneView& sv, const TravRay& 
     }
 #endif
     return (ax | ay | az) && octree_crack_planes(sv.oct->grid, r.o, r.d, ts.bt, ax, ay, az);
-#endif
 }
 
 // counts a query octree_flag sent to the octree: ties[0] (bit 0) or ties[6] (crack)

@@ -44,3 +44,15 @@ def assemble(tiles: Sequence, rows: Sequence[np.ndarray], frame):
         else:
             frame[r] = np.asarray(t)[:n]
     return frame
+
+
+def placement(devices: Sequence[dict], backend) -> dict:
+    """What a multi-rank run ran on, from every rank's device identity
+    ({"pci": domain:bus:device, "uuid": ...}, rank order): ``n_gpus`` counts
+    DISTINCT devices, so ranks that share a GPU (the gloo rehearsal) are not
+    reported as more GPUs; ``ranks`` is the process count; ``rehearsal`` is
+    true when some ranks share a device.  ``backend`` is None for a plain
+    single-process run (no process group)."""
+    distinct = len({(d["pci"], d.get("uuid", "")) for d in devices})
+    return {"n_gpus": distinct, "ranks": len(devices), "dist_backend": backend,
+            "devices": [d["pci"] for d in devices], "rehearsal": distinct < len(devices)}
