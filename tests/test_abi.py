@@ -120,3 +120,13 @@ def test_scene_options_are_checked_before_any_device_work():
         for good in ("builder=lbvh, leaf_max=4", {"collapse": "sah", "ploc_radius": 8}, "", None, "row_occ=4"):
             with pytest.raises(tm.TmptError, match="device"):
                 tm.Scene(tris, options=good)
+
+
+def test_stats_mirror_matches_the_struct():
+    """RenderStats (the Python face of tmpt_stats) carries every field of the
+    ctypes mirror except the reserved words, in order, so Scene.stats() can
+    build it without a GPU render having run."""
+    fields = [f for f, _ in tm._Stats._fields_ if not f.startswith("reserved")]
+    assert list(tm.RenderStats._fields if hasattr(tm.RenderStats, "_fields") else
+                tm.RenderStats.__dataclass_fields__) == fields
+    assert "tie_path" in fields

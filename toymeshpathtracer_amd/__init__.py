@@ -538,7 +538,7 @@ class Scene:
     def stats(self) -> RenderStats:
         s = _Stats()
         _check(_stats(self._h, ctypes.byref(s)), "stats")
-        return RenderStats(*[getattr(s, f) for f, _ in _Stats._fields_])
+        return RenderStats(*[getattr(s, f) for f, _ in _Stats._fields_ if not f.startswith("reserved")])
 
 
 def render_multi(tris: np.ndarray, camera: "Camera", width: int, height: int, spp: int, devices,
