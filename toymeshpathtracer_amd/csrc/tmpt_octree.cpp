@@ -258,18 +258,40 @@ static float plane_dist(const OctGrid& g, int k, float x, float& j)
     return fabsf(fmaf(-j, g.cell[k], rel));
 }
 
+// Triangles the reference's octree may not hold where a ray hits them (DESIGN.md
+// section 2, "the derived bound"): (F1) all three vertices within 2 band of one
+// plane -- the triangle can lie in a crack, in no leaf at all; (F2) a triangle
+// nearly parallel to a plane family that comes within band of one of its
+// planes: its plane leaves the 2-band slab around that plane only beyond
+// `reach` of a point inside it (sin(angle) * reach <= 2 band), so near such a
+// point it may meet neither leaf either side of the crack robustly.
 int32_t octree_flat_triangles(const float* tris9, int32_t n, const OctGrid& g, std::vector<uint8_t>& flat)
 {
     flat.assign((size_t)n, 0);
     int32_t count = 0;
     for (int32_t i = 0; i < n; ++i) {
         const float* v = tris9 + 9 * (size_t)i;
-        for (int k = 0; k < 3 && !flat[(size_t)i]; ++k) {
+        for (int k = 0; k < 3 && !flat[(size_t)i]; ++k) {  // F1
             float j0, j1, j2;
             const float d0 = plane_dist(g, k, v[k], j0), d1 = plane_dist(g, k, v[3 + k], j1),
                         d2 = plane_dist(g, k, v[6 + k], j2);
             const float lim = 2.0f * g.band[k];
             if (j0 == j1 && j1 == j2 && d0 <= lim && d1 <= lim && d2 <= lim) flat[(size_t)i] = 1;
+        }
+        if (!flat[(size_t)i]) {  // F2
+            const double e1[3] = {(double)v[3] - v[0], (double)v[4] - v[1], (double)v[5] - v[2]};
+            const double e2[3] = {(double)v[6] - v[0], (double)v[7] - v[1], (double)v[8] - v[2]};
+            const double nr[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                                  e1[0] * e2[1] - e1[1] * e2[0]};
+            const double len = std::sqrt(nr[0] * nr[0] + nr[1] * nr[1] + nr[2] * nr[2]);
+            for (int k = 0; k < 3 && len > 0.0 && !flat[(size_t)i]; ++k) {
+                const double nk = std::fabs(nr[k]) / len, sin_a = std::sqrt(std::max(0.0, 1.0 - nk * nk));
+                if (sin_a * (double)g.reach > 2.0 * (double)g.band[k]) continue;
+                const double lo = std::min({(double)v[k], (double)v[3 + k], (double)v[6 + k]}) - g.band[k];
+                const double hi = std::max({(double)v[k], (double)v[3 + k], (double)v[6 + k]}) + g.band[k];
+                // a plane r0 + j cell inside [lo, hi]
+                if (std::floor((hi - g.r0[k]) / g.cell[k]) >= std::ceil((lo - g.r0[k]) / g.cell[k])) flat[(size_t)i] = 1;
+            }
         }
         count += flat[(size_t)i];
     }
