@@ -30,5 +30,7 @@ find $out -name "*.db" -delete
 timeout -k 10 400 python3 bench.py --config sponza4k --steps 2 --warmup 1 --no-cpu > $out/bench_sponza4k.json 2> $out/bench_sponza4k.err || { echo "4k rc=$?"; tail -5 $out/bench_sponza4k.err; exit 1; }
 python3 -c "import json; d=json.load(open('$out/bench_sponza4k.json')); print('4k', d['value'], d['ms_per_step'])"
 timeout -k 10 400 python3 bench.py --gpus 2 --dist-backend gloo --steps 2 --warmup 1 > $out/gloo2.json 2> $out/gloo2.err || { echo "gloo2 rc=$?"; tail -20 $out/gloo2.err; exit 1; }
-python3 -c "import json; d=json.load(open('$out/gloo2.json')); print('gloo2', d['value'], d['n_gpus'])"
+python3 -c "import json; d=json.load(open('$out/gloo2.json')); print('gloo2', d['value'], d['n_gpus'], d['ranks'], d['rehearsal'], d['devices'])"
+timeout -k 10 400 python3 bench.py --gpus 4 --dist-backend gloo --steps 2 --warmup 1 > $out/gloo4.json 2> $out/gloo4.err || { echo "gloo4 rc=$?"; tail -20 $out/gloo4.err; exit 1; }
+python3 -c "import json; d=json.load(open('$out/gloo4.json')); print('gloo4', d['value'], d['n_gpus'], d['ranks'], d['rehearsal'], d['devices'])"
 echo session-done
