@@ -41,6 +41,7 @@ constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
 constexpr int kTopNodes = 120;  // BVH4 nodes held in LDS per path block (7.5 KB)
+constexpr int kTopNodes5 = 112;  // the same in the 5-wave sample kernel (7 KB: 32 KB per block in all)
 
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x

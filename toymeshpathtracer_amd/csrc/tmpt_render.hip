@@ -1181,7 +1181,11 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     __shared__ uint32_t s_stack[SL * BLOCK];
     // SAMP 3, 4 (shadow-free speculation): no light terms, no pending next ray
     __shared__ float s_light[SAMP >= 3 ? 1 : kMaxDepth * BLOCK];
-    __shared__ float s_next[SAMP >= 3 ? 1 : 6 * BLOCK];
+    // OCC 5 (5 waves per SIMD, <= 32 KB of LDS per block): only the scattered
+    // ray's direction is kept while its bounce's shadow query runs -- its
+    // origin is the shadow ray's (r.o)
+    constexpr bool NEXT3 = OCC >= 5;
+    __shared__ float s_next[SAMP >= 3 ? 1 : (NEXT3 ? 3 : 6) * BLOCK];
     if (SAMP == 4) {
         // The chaser role goes by arrival, not by blockIdx: the first nchase
         // blocks to START take it, so every chaser is resident by construction
@@ -1205,7 +1209,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
     __shared__ uint8_t s_pair[HELP ? BLOCK : 1];
     {  // the top BVH4 levels (nodes are numbered level by level) in LDS
         // HELP: 4 nodes fewer, so s_pair keeps the block at 4 per CU
-        constexpr int kTop = HELP ? kTopNodes - 4 : kTopNodes;
+        constexpr int kTop = OCC >= 5 ? kTopNodes5 : (HELP ? kTopNodes - 4 : kTopNodes);
         __shared__ uint4 s_top[kTop * 4];
         const uint32_t ntop = (uint32_t)min(kTop, sv.n_nodes4);
         const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
@@ -1592,8 +1596,12 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         f3 nd = normalize(target - pos);
                         ++depth;
                         if (SAMP < 3 && lc > 0.0f && !(SAMP == 2 && pc.rs_noshadow)) {
-                            nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
-                            nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
+                            if (NEXT3) {
+                                nxt[0] = nd.x; nxt[LS] = nd.y; nxt[2 * LS] = nd.z;
+                            } else {
+                                nxt[0] = pos.x; nxt[LS] = pos.y; nxt[2 * LS] = pos.z;
+                                nxt[3 * LS] = nd.x; nxt[4 * LS] = nd.y; nxt[5 * LS] = nd.z;
+                            }
                             start = true;  // shadow query toward the light
                             sany = true;
                             so = pos;
@@ -1624,8 +1632,13 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                     if (ts.best >= 0) light[(depth - 1) * LS] = 0.0f;
                     if (depth < (uint32_t)kMaxDepth) {
                         start = true;  // the scattered ray of that bounce
-                        so = mk(nxt[0], nxt[LS], nxt[2 * LS]);
-                        sd = mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
+                        if (NEXT3) {  // the shadow ray started at the hit point
+                            so = r.o;
+                            sd = mk(nxt[0], nxt[LS], nxt[2 * LS]);
+                        } else {
+                            so = mk(nxt[0], nxt[LS], nxt[2 * LS]);
+                            sd = mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
+                        }
                     } else {
                         finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
                     }
@@ -1650,7 +1663,7 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
                         light[(depth - 1) * LS] = -light[(depth - 1) * LS];
                         sany = false;
                         if (depth < (uint32_t)kMaxDepth) {
-                            sd = mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
+                            sd = NEXT3 ? mk(nxt[0], nxt[LS], nxt[2 * LS]) : mk(nxt[3 * LS], nxt[4 * LS], nxt[5 * LS]);
                         } else {
                             start = false;
                             finish = true;  // kMaxDepth hits, colour stays 0 (main.cpp:88-89)
@@ -2770,6 +2783,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms);
     // sample seeding 220.4 -> 218.2 ms at N=1, 29.4 -> 29.0 ms at 1/8
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
+    // the 5-wave sample kernel (OCC 5): 32 KB of LDS per block -- a 12-entry
+    // LDS stack, the scattered ray's direction only, kTopNodes5 top nodes
+    constexpr int kPathSL5 = 12;
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
     // kernel keeps its register allocation)
@@ -2934,7 +2950,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     if (!a.jt && !count && !prof && s.oct_view && o.tie_rule == 0)
         fn = help ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>
                   : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>;
-    const size_t ovf_words = (size_t)grid * kBlk * (kStackTotal - kPathSL);
+    // (room for the 5-wave sample kernel's lanes and its shorter LDS stack too)
+    const size_t ovf_words = std::max((size_t)grid * kBlk * (kStackTotal - kPathSL),
+                                      (size_t)grid * 5 / 4 * kBlk * (kStackTotal - kPathSL5));
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
     const size_t reg_words = ordered ? 2 * (size_t)kSimdKeys + 64 + (size_t)P : 0;  // + claim words
@@ -3026,6 +3044,19 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
         else if (fn == fn_default && a.jt && !count && !soa && s.oct_view && o.tie_rule == 0)
             fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
+#ifdef TMPT_V_OCC5
+        if (redo) fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>;
+#endif
+        // the launch's grid is the launched kernel's co-resident block count
+        // (the deferred re-traces' completion count relies on it)
+        const int grid_main = fn_main == fn ? grid : occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
+#ifdef TMPT_V_OCC5
+        if (getenv("TMPT_V_PRINT_GRID")) fprintf(stderr, "grid %d grid_main %d\n", grid, grid_main);
+#endif
+        if ((size_t)grid_main * kBlk * (kStackTotal - (grid_main > grid ? kPathSL5 : kPathSL)) > ovf_words) {
+            set_error("tmpt_render: internal: stack spill area sized for fewer lanes");
+            return -1;
+        }
         s.tie_path = !(s.oct_view && o.tie_rule == 0) ? 0 : redo ? 2 : redo_nomem ? 3 : 1;
         s.path_launches = 1;
         for (int attempt = 0;; ++attempt) {
@@ -3036,7 +3067,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             pc.redo_lanes = (uint32_t)std::max(1, std::min(64, o.redo_lanes));
             if (redo) TMPT_HIP(hipMemsetAsync(s.redo, 0xFF, sizeof(uint2) * (size_t)s.redo_cap, s.stream));
             TMPT_HIP(hipEventRecord(s.path_ev[2], s.stream));
-            fn_main<<<grid, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, (uint32_t*)s.ws, d_counters);
+            fn_main<<<grid_main, kBlk, 0, s.stream>>>(view(s), as, pc, d_out, (uint32_t*)s.ws, d_counters);
             TMPT_HIP(hipGetLastError());
             TMPT_HIP(hipEventRecord(s.path_ev[3], s.stream));
             if (!redo) break;
