@@ -113,7 +113,7 @@ def test_scene_options_are_checked_before_any_device_work():
     tris = np.zeros((1, 9), np.float32)
     for bad, msg in (("bogus=1", "unknown option"), ("leaf_max=0", "out of range"), ("leaf_max=x", "bad value"),
                      ("builder=kd", "bad value"), ("sample_block=3", "power of two"), ("leaf_max", "no value"),
-                     ("pilot=1.5", "integer"), ("row_occ=2", "0 \\(by load\\), 4 or 5")):
+                     ("pilot=1.5", "integer"), ("row_occ=2", "0 \\(auto\\), 4 or 5"), ("path_waves=3", "0 \\(auto\\), 4 or 5")):
         with pytest.raises(tm.TmptError, match=msg):
             tm.Scene(tris, options=bad)
     if tm.device_count() == 0:

@@ -126,6 +126,7 @@ const OptionDef kOptions[] = {
     {"redo_cap", false, 0, 1 << 30, &Options::redo_cap, nullptr, nullptr},
     {"redo_inline", false, 0, 1, &Options::redo_inline, nullptr, nullptr},
     {"redo_lanes", false, 1, 64, &Options::redo_lanes, nullptr, nullptr},
+    {"path_waves", false, 0, 5, &Options::path_waves, nullptr, nullptr},
     {"rowspec", false, 0, 1, &Options::rowspec, nullptr, nullptr},
     {"rowspec_wmax", false, 0, 16384, &Options::rowspec_wmax, nullptr, nullptr},
     {"rowspec_windows", false, 0, 32, &Options::rowspec_windows, nullptr, nullptr},
@@ -171,8 +172,8 @@ int options_set(Options& o, const char* key, double v, bool allow_build)
             set_error(std::string("option '") + key + "' takes an integer");
             return -22;
         }
-        if (strcmp(key, "row_occ") == 0 && v != 0 && v != 4 && v != 5) {  // waves per SIMD: by load, 4 or 5
-            set_error("option 'row_occ' takes 0 (by load), 4 or 5");
+        if ((strcmp(key, "row_occ") == 0 || strcmp(key, "path_waves") == 0) && v != 0 && v != 4 && v != 5) {
+            set_error(std::string("option '") + key + "' takes 0 (auto), 4 or 5");  // waves per SIMD
             return -22;
         }
         if ((strcmp(key, "sample_block") == 0 || strcmp(key, "wf_bins") == 0) && v > 0 &&

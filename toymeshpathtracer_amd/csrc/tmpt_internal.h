@@ -41,7 +41,12 @@ constexpr int kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1u;
 constexpr int kLeafMaxTris = 16;
 constexpr int kTopNodes = 120;  // BVH4 nodes held in LDS per path block (7.5 KB)
-constexpr int kTopNodes5 = 112;  // the same in the 5-wave sample kernel (7 KB: 32 KB per block in all)
+// The same in the 5-wave path kernels (OCC 5): 5 KB, so a block's LDS is 30 KB
+// (12-entry stack 12 KB, light terms 10 KB, pending ray 3 KB, top nodes 5 KB).
+// Five such blocks fit a CU; with 104 nodes (31.5 KB) they did not (the
+// occupancy API still said 5, and the launch's tail waited for blocks that
+// were never resident), 72-96 nodes measured alike.
+constexpr int kTopNodes5 = 80;
 
 struct alignas(16) TriPre {
     float4 a;  // v0.xyz, e1.x
@@ -218,6 +223,7 @@ struct Options {
     int redo_cap = 0;         // test hook: the redo list's capacity in entries (0 = auto; a small one
                               // overflows, and the frame is rendered again with the list grown)
     int redo_lanes = 4;       // tie_defer: lanes per wave that take re-traces in the launch's tail
+    int path_waves = 0;       // sample seeding, deferred ties: path-kernel waves per SIMD (0 = auto = 5, 4 or 5)
     int redo_inline = 1;      // test hook: 0 = the deferring kernel's waves leave every dropped sample
                               // to the k_redo launch (its fallback) instead of tracing them in their tail
 };

@@ -3044,15 +3044,14 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
         else if (fn == fn_default && a.jt && !count && !soa && s.oct_view && o.tie_rule == 0)
             fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
-#ifdef TMPT_V_OCC5
-        if (redo) fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>;
-#endif
+        // five waves per SIMD (option path_waves; the 30-KB LDS layout of
+        // OCC 5, 96 VGPRs): bench frame, k_path ms, 4 / 5 waves: N=1
+        // 186.2 / 171.4-172.6
+        if (redo && o.path_waves != 4)
+            fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>;
         // the launch's grid is the launched kernel's co-resident block count
         // (the deferred re-traces' completion count relies on it)
         const int grid_main = fn_main == fn ? grid : occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
-#ifdef TMPT_V_OCC5
-        if (getenv("TMPT_V_PRINT_GRID")) fprintf(stderr, "grid %d grid_main %d\n", grid, grid_main);
-#endif
         if ((size_t)grid_main * kBlk * (kStackTotal - (grid_main > grid ? kPathSL5 : kPathSL)) > ovf_words) {
             set_error("tmpt_render: internal: stack spill area sized for fewer lanes");
             return -1;
