@@ -2415,6 +2415,9 @@ namespace {
 
 constexpr int kBlk = 256;
 constexpr int kSL = 16;  // LDS stack entries per lane
+// the 5-wave path kernels (OCC 5): 30 KB of LDS per block -- a 12-entry LDS
+// stack, the scattered ray's direction only, kTopNodes5 top nodes
+constexpr int kPathSL5 = 12;
 
 int occupancy_grid(const void* fn, int block, size_t dyn_lds, int device)
 {
@@ -2783,9 +2786,6 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms);
     // sample seeding 220.4 -> 218.2 ms at N=1, 29.4 -> 29.0 ms at 1/8
     constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
-    // the 5-wave sample kernel (OCC 5): 32 KB of LDS per block -- a 12-entry
-    // LDS stack, the scattered ray's direction only, kTopNodes5 top nodes
-    constexpr int kPathSL5 = 12;
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
     // kernel keeps its register allocation)
@@ -2813,7 +2813,13 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         fn = prof >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 2, 0, 1>
                        : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 1, 0, 1>;
 #endif
-    const int grid = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    // Sample seeding's path kernels run 5 waves per SIMD (OCC 5: the 30-KB LDS
+    // layout, 96 VGPRs; option path_waves): the lanes below are theirs
+    const bool waves5 = a.jt && !count && !prof && !soa && o.path_waves != 4;
+    const int grid = occupancy_grid(
+        waves5 ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>
+               : (const void*)fn,
+        kBlk, 0, s.device);
     // Sample seeding: the work units are (pixel, block of blk samples).  The
     // block is the largest power of two up to 8 that still leaves >=
     // kUnitsPerLane units per resident lane.  Bench frame (1-row bands,
@@ -3040,19 +3046,22 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         // (the deferring kernel keeps the first triangle met on a tie and flags
         // it: only the redo pass gives those samples their answer)
         // (with the octree but no deferral: the leaf only flags ties, TIES 2)
+        // five waves per SIMD (waves5, option path_waves; the 30-KB LDS layout
+        // of OCC 5, 96 VGPRs): bench frame, k_path ms, 4 / 5 waves, same box:
+        // N=1 185.6 / 171.0, 1/2 94.3 / 87.7
         PathFn fn_main = fn;
-        if (redo) fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
+        if (redo)
+            fn_main = waves5 ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>
+                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 1>;
         else if (fn == fn_default && a.jt && !count && !soa && s.oct_view && o.tie_rule == 0)
-            fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
-        // five waves per SIMD (option path_waves; the 30-KB LDS layout of
-        // OCC 5, 96 VGPRs): bench frame, k_path ms, 4 / 5 waves: N=1
-        // 186.2 / 171.4-172.6
-        if (redo && o.path_waves != 4)
-            fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>;
+            fn_main = waves5 ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 2>
+                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
+        else if (waves5 && fn == fn_default)
+            fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1>;
         // the launch's grid is the launched kernel's co-resident block count
         // (the deferred re-traces' completion count relies on it)
-        const int grid_main = fn_main == fn ? grid : occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
-        if ((size_t)grid_main * kBlk * (kStackTotal - (grid_main > grid ? kPathSL5 : kPathSL)) > ovf_words) {
+        const int grid_main = occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
+        if ((size_t)grid_main * kBlk * (kStackTotal - kPathSL5) > ovf_words) {
             set_error("tmpt_render: internal: stack spill area sized for fewer lanes");
             return -1;
         }
@@ -3224,8 +3233,13 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     // is not needed (option row_flag_leaves 0 keeps it, for A/B)
     const bool flag = s.oct_view && o.tie_rule == 0 && o.row_flag_leaves;
     using RsFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>);
-    const RsFn fn2 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2, false, 2>
-                          : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>;
+    // the chain's full re-trace at 5 waves per SIMD (option path_waves, as the
+    // sample kernels: the 30-KB LDS layout of OCC 5)
+    const bool w5 = o.path_waves != 4;
+    const RsFn fn2 = flag ? (w5 ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 2, false, 2>
+                                : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2, false, 2>)
+                          : (w5 ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 2>
+                                : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 2>);
     RsFn fn4 = flag ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4, false, 2>
                     : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, kRsOcc3, kSparse, 0, 0, 4>;
     // the workers at 4 waves per SIMD (no spills) for light loads (option row_occ)
@@ -3279,7 +3293,7 @@ int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned lo
     nw = std::max(2, std::min(kRssT - 1, nw));
     if (o.rowspec_windows > 0) nw = std::min(kRssT - 1, o.rowspec_windows);
     const uint32_t na = (uint32_t)(((uint64_t)W * spp * 14u + R) >> 14) + 1u;
-    const size_t ovf_words = (size_t)std::max(grid, grid2) * kBlk * (kStackTotal - kPathSL);
+    const size_t ovf_words = std::max((size_t)grid * (kStackTotal - kPathSL), (size_t)grid2 * (kStackTotal - kPathSL5)) * kBlk;
     const size_t head_words = (size_t)kSeg * kCtr;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t b_res = al((size_t)rows * T * R * 8), b_slots = al((size_t)rows * (T + 1) * 8),
