@@ -2843,7 +2843,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     const bool pass = a.jt && (a.smp_begin > 0 || a.smp_end < a.spp);
     const int64_t s0 = a.smp_begin, s1 = a.smp_end;
     if (a.jt) {
-        constexpr int64_t kUnitsPerLane = 15;
+        // (15 units per 4-wave lane; with 5 waves per SIMD a quarter more lanes
+        // share the work, and 12 per lane picks the same blocks as 15 did:
+        // 8, 8, 8, 4 at N = 1, 2, 4, 8 -- round 6, profiles/r06_experiments/occ5/)
+        const int64_t kUnitsPerLane = waves5 ? 12 : 15;
         const int64_t lanes0 = (int64_t)grid * kBlk;
         blk = 1u;
         while ((int64_t)blk * 2 <= 8 && blk * 2u <= (uint32_t)(s1 - s0) &&
@@ -3027,13 +3030,17 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
         // triangle met on a tie, flagged) and the launch's waves trace the
         // dropped samples in their tail (k_redo the rest).  Only when no camera
         // ray needs the root-box test (root_check = 0).  Auto: at >= 192 samples
-        // per resident lane, where the tail hides the re-traces -- bench frame,
-        // k_path ms, base (no octree) / ties settled inline / deferred: N=1
-        // 184.8 / 190.2 / 185.3, 1/2 93.1 / 96.3 / 94.9, 1/4 47.7 / 49.4 /
-        // 49.8, 1/8 24.6 / 25.5 / 27.1
+        // per resident lane (4 waves per SIMD), where the tail hides the
+        // re-traces -- bench frame, k_path ms, base (no octree) / ties settled
+        // inline / deferred: N=1 184.8 / 190.2 / 185.3, 1/2 93.1 / 96.3 / 94.9,
+        // 1/4 47.7 / 49.4 / 49.8, 1/8 24.6 / 25.5 / 27.1;
+        // with 5 waves per SIMD the deferring kernel wins down to the 1/8
+        // shard (51 samples per lane; inline / deferred with its block rule:
+        // 1/4 47.3 / 45.9, 1/8 24.3 / 24.2 ms), so from 48 per lane
+        // (profiles/r06_experiments/occ5/ab_low_rules.log)
         const bool defer = a.jt && !count && !prof && !soa && pc.sbuf && a.root_check == 0 && o.tie_defer != 0 &&
                            !oct_shadow &&
-                           (o.tie_defer > 0 || a.slots * (int64_t)a.spp >= 192 * lanes);
+                           (o.tie_defer > 0 || a.slots * (int64_t)a.spp >= (waves5 ? 48 : 192) * lanes);
         bool redo = defer && s.oct_view && o.tie_rule == 0;
         if (redo && o.redo_cap > 0 && s.redo_cap != (uint32_t)o.redo_cap) free_redo(s);  // the test hook's size
         if (redo && s.redo_cap == 0) {
