@@ -2816,9 +2816,12 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // Sample seeding's path kernels run 5 waves per SIMD (OCC 5: the 30-KB LDS
     // layout, 96 VGPRs; option path_waves): the lanes below are theirs
     const bool waves5 = a.jt && !count && !prof && !soa && o.path_waves != 4;
+    // (pixel seeding's too: every one of its instantiations below)
+    const bool waves5p = !a.jt && !count && !prof && o.path_waves != 4;
     const int grid = occupancy_grid(
         waves5 ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>
-               : (const void*)fn,
+        : waves5p ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse>
+                  : (const void*)fn,
         kBlk, 0, s.device);
     // Sample seeding: the work units are (pixel, block of blk samples).  The
     // block is the largest power of two up to 8 that still leaves >=
@@ -2954,11 +2957,17 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     if (oct_shadow) help = 0;  // the helpers' shadow answers are not checked
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
     if (o.pair >= 0) pair = o.pair;
-    if (help) fn = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
+    if (help)
+        fn = waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 1>
+                     : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
+    else if (waves5p)
+        fn = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse>;
     // pixel seeding with the octree there: the leaves only flag ties (TIES 2)
     if (!a.jt && !count && !prof && s.oct_view && o.tie_rule == 0)
-        fn = help ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>
-                  : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>;
+        fn = help ? (waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 1, 0, false, 2>
+                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>)
+                  : (waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 0, false, 2>
+                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>);
     // (room for the 5-wave sample kernel's lanes and its shorter LDS stack too)
     const size_t ovf_words = std::max((size_t)grid * kBlk * (kStackTotal - kPathSL),
                                       (size_t)grid * 5 / 4 * kBlk * (kStackTotal - kPathSL5));
