@@ -255,8 +255,10 @@ int tmpt_scene_create(const float* tris, int32_t n, int32_t device, tmpt_scene**
  *                    their main loop is done (-1 = auto, 0 = off: ties settled in the
  *                    main loop, 1 = on); the image and ray counts are the same either way
  *   redo_lanes       tie_defer: lanes per wave that take the re-traces (1..64, default 4)
- *   path_waves       tie_defer: waves per SIMD of the deferring sample kernel (0 = auto = 5, 4 or 5;
- *                    5: a 12-entry LDS stack and 80 LDS top nodes, 30 KB of LDS and 96 VGPRs per lane)
+ *   path_waves       waves per SIMD of the persistent path kernels (0 = auto, 4 or 5; 5: a 12-entry LDS
+ *                    stack and 80 LDS top nodes, 30 KB of LDS per block and 96 VGPRs per lane).  Auto:
+ *                    5 in sample seeding and the row engine's re-trace, 5 in pixel seeding from 3 pixels
+ *                    per 4-wave lane
  *   redo_cap         test hook (0 = auto): the capacity of tie_defer's sample list; a
  *                    frame that overflows it is rendered again with the list grown
  *   redo_inline      test hook (1): 0 leaves every dropped sample to the second launch

@@ -223,7 +223,8 @@ struct Options {
     int redo_cap = 0;         // test hook: the redo list's capacity in entries (0 = auto; a small one
                               // overflows, and the frame is rendered again with the list grown)
     int redo_lanes = 4;       // tie_defer: lanes per wave that take re-traces in the launch's tail
-    int path_waves = 0;       // sample seeding, deferred ties: path-kernel waves per SIMD (0 = auto = 5, 4 or 5)
+    int path_waves = 0;       // path-kernel waves per SIMD (0 = auto: 5 in sample seeding, in pixel seeding
+                              // from 3 pixels per 4-wave lane; 4 or 5)
     int redo_inline = 1;      // test hook: 0 = the deferring kernel's waves leave every dropped sample
                               // to the k_redo launch (its fallback) instead of tracing them in their tail
 };

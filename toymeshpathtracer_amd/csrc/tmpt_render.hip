@@ -2816,8 +2816,15 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // Sample seeding's path kernels run 5 waves per SIMD (OCC 5: the 30-KB LDS
     // layout, 96 VGPRs; option path_waves): the lanes below are theirs
     const bool waves5 = a.jt && !count && !prof && !soa && o.path_waves != 4;
-    // (pixel seeding's too: every one of its instantiations below)
-    const bool waves5p = !a.jt && !count && !prof && o.path_waves != 4;
+    // Pixel seeding's instantiations too, but only with several pixels per
+    // lane: at low load a pixel's sample chain is the frame's critical path
+    // and a fifth wave on the SIMD slows every chain (whole renders, 4 / 5
+    // waves: N=1 207.2 / 197.6 ms, 1/2 116.9 / 113.9, 1/4 63.6 / 65.7, 1/8
+    // 36.2 / 39.1; profiles/r06_experiments/occ5/ab_pixel_waves.log), so from
+    // 3 pixels per 4-wave lane (option path_waves 5 forces it, 4 keeps 4)
+    const int grid4 = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const bool waves5p = !a.jt && !count && !prof &&
+                         (o.path_waves == 5 || (o.path_waves == 0 && a.slots >= 3 * (int64_t)grid4 * kBlk));
     const int grid = occupancy_grid(
         waves5 ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>
         : waves5p ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse>
