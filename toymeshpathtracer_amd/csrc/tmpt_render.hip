@@ -1889,12 +1889,16 @@ __global__ void __launch_bounds__(BLOCK, OCC) k_path(SceneView sv, RenderArgs a,
         // is left to k_redo (stats redo_late = 0, asserted by the GPU suite).
         // kRedoGuard is only a deadlock guard for a dispatcher that holds
         // blocks back behind resident ones (the GPU shared with another
-        // process): after 250 ms in which neither the list nor the count of
+        // process): after 20 ms in which neither the list nor the count of
         // waves past their main loop changed, the wave leaves its tickets to
         // k_redo.  A wave waits through the frame's tail only, and the count
-        // changes every time a wave leaves its main loop.  (Counting started waves instead of
-        // the grid cost 2 % in register allocation, measured.)
-        constexpr uint64_t kRedoGuard = 25000000;  // s_memrealtime ticks (100 MHz): 250 ms
+        // changes every time a wave leaves its main loop (the main loops end
+        // within ~2 ms of each other), so a working launch never sees 20 ms
+        // without a change; round 5's 250 ms cost each frame of 4 processes
+        // sharing one GPU (the gloo rehearsal) a quarter second once the
+        // deferral ran at their shard size.  (Counting started waves instead
+        // of the grid cost 2 % in register allocation, measured.)
+        constexpr uint64_t kRedoGuard = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
         const unsigned long long waves = (unsigned long long)gridDim.x * (BLOCK / 64);
         // pc.redo_lanes lanes of the wave take tickets: a re-trace is one
         // lane's whole path, so fewer per wave spread them over more waves
