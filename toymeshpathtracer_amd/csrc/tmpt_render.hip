@@ -2826,14 +2826,15 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // waves: N=1 207.2 / 197.6 ms, 1/2 116.9 / 113.9, 1/4 63.6 / 65.7, 1/8
     // 36.2 / 39.1; profiles/r06_experiments/occ5/ab_pixel_waves.log), so from
     // 3 pixels per 4-wave lane (option path_waves 5 forces it, 4 keeps 4)
+    // (every OCC 5 instantiation has the same LDS and VGPR footprint, so one
+    // of them gives the 5-wave grid)
     const int grid4 = occupancy_grid((const void*)fn, kBlk, 0, s.device);
+    const int grid5 = occupancy_grid(
+        (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>, kBlk, 0,
+        s.device);
     const bool waves5p = !a.jt && !count && !prof &&
                          (o.path_waves == 5 || (o.path_waves == 0 && a.slots >= 3 * (int64_t)grid4 * kBlk));
-    const int grid = occupancy_grid(
-        waves5 ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 1>
-        : waves5p ? (const void*)k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse>
-                  : (const void*)fn,
-        kBlk, 0, s.device);
+    const int grid = waves5 || waves5p ? grid5 : grid4;
     // Sample seeding: the work units are (pixel, block of blk samples).  The
     // block is the largest power of two up to 8 that still leaves >=
     // kUnitsPerLane units per resident lane.  Bench frame (1-row bands,
@@ -2979,9 +2980,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>)
                   : (waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 0, false, 2>
                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>);
-    // (room for the 5-wave sample kernel's lanes and its shorter LDS stack too)
-    const size_t ovf_words = std::max((size_t)grid * kBlk * (kStackTotal - kPathSL),
-                                      (size_t)grid * 5 / 4 * kBlk * (kStackTotal - kPathSL5));
+    // stack spill areas for either kind of kernel's lanes (4 waves, 16 LDS
+    // entries; 5 waves, 12)
+    const size_t ovf_words = std::max((size_t)grid4 * (kStackTotal - kPathSL),
+                                      (size_t)std::max(grid4, grid5) * (kStackTotal - kPathSL5)) * kBlk;
     const size_t head_words = (size_t)kSeg * kCtr;
     const size_t hist_words = ordered ? radix_sort_hist_words((int32_t)P) : 0;
     const size_t reg_words = ordered ? 2 * (size_t)kSimdKeys + 64 + (size_t)P : 0;  // + claim words
@@ -3087,7 +3089,7 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
             fn_main = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1>;
         // the launch's grid is the launched kernel's co-resident block count
         // (the deferred re-traces' completion count relies on it)
-        const int grid_main = occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
+        int grid_main = occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
         if ((size_t)grid_main * kBlk * (kStackTotal - kPathSL5) > ovf_words) {
             set_error("tmpt_render: internal: stack spill area sized for fewer lanes");
             return -1;
@@ -3118,7 +3120,10 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                 // the same samples) or, failing that, render with the exact kernel
                 if (!(n < (1ull << 31) && alloc_redo(s, (int64_t)n))) {
                     redo = false;
-                    fn_main = k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
+                    fn_main = waves5
+                                  ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 1, false, 2>
+                                  : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, false, 2>;
+                    grid_main = occupancy_grid((const void*)fn_main, kBlk, 0, s.device);
                     s.redo_samples = 0;
                     s.tie_path = 3;
                 }
