@@ -984,6 +984,44 @@ def test_sample_mode_bench_frame_full_spp_vs_oracle(gpu, sponza_path):
     assert diff[0].size == 0, f"{diff[0].size} pixels differ, first at {list(zip(*diff))[:5]}"
 
 
+@pytest.mark.parametrize("seed", ["sample", "pixel"])
+def test_path_waves_same_frame_and_rays(gpu, sponza_path, seed):
+    """The 5-wave path kernels (option path_waves 5: a 12-entry LDS stack,
+    the pending ray's direction only, 80 LDS top nodes) render the same
+    frame and ray count as the 4-wave ones (path_waves 4), in sample seeding
+    (deferred ties, whole frame and a 1/8 shard) and pixel seeding (cost-
+    ordered passes, with and without the shadow offload), and the tie_path
+    stat says which answer path ran."""
+    tris, bmin, bmax = tm.load_scene(sponza_path)
+    w, h, spp = 480, 270, 16
+    cam = tm.Camera.for_scene(bmin, bmax, w, h, is_sponza=True)
+    sd = tm.SEED_SAMPLE if seed == "sample" else tm.SEED_PIXEL
+    with tm.Scene(tris, bounds=(bmin, bmax)) as sc:
+        for shards in (1, 8):
+            kw = dict(seed_mode=sd, band_rows=1, shard=0, num_shards=shards)
+            out = {}
+            for waves in (4, 5):
+                sc.set_option("path_waves", waves)
+                if seed == "sample":
+                    sc.set_option("tie_defer", 1)
+                    img, rays = sc.trace_image(cam, w, h, spp, **kw)
+                    st = sc.stats()
+                    assert st.tie_path == 2 and st.redo_samples > 0 and st.redo_late == 0
+                    out[waves] = (img, rays)
+                else:
+                    for help_ in (0, 1):
+                        sc.set_option("help", help_)
+                        img, rays = sc.trace_image(cam, w, h, spp, **kw)
+                        assert sc.stats().tie_path == 1
+                        out[(waves, help_)] = (img, rays)
+                    sc.set_option("help", -1)
+            first = next(iter(out.values()))
+            for k, (img, rays) in out.items():
+                assert rays == first[1] and np.array_equal(img, first[0]), (shards, k)
+        sc.set_option("path_waves", 0)
+        sc.set_option("tie_defer", -1)
+
+
 @pytest.mark.parametrize("shards", [1, 8])
 def test_tie_defer_same_frame_and_rays(gpu, sponza_path, shards):
     """Deferred ties (option tie_defer): the sample kernel's main loop, built
