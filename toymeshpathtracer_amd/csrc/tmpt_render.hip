@@ -875,7 +875,19 @@ __global__ void __launch_bounds__(kSeg) k_wf_advance(WfState s, int parity, int 
 #ifndef TMPT_RSS_T
 #define TMPT_RSS_T 8
 #endif
-constexpr int kRssT = TMPT_RSS_T;  // live pixel windows per row at most kRssT - 1 (plus the demand slot)
+constexpr int kRssT = TMPT_RSS_T;
+#ifndef TMPT_PATH_STEPS
+#define TMPT_PATH_STEPS 16
+#endif
+#ifndef TMPT_PIX_STEPS
+#define TMPT_PIX_STEPS 24
+#endif
+#ifndef TMPT_SHADE_MIN
+#define TMPT_SHADE_MIN 16
+#endif
+#ifndef TMPT_SPARSE
+#define TMPT_SPARSE 2
+#endif  // live pixel windows per row at most kRssT - 1 (plus the demand slot)
 static_assert(kRssT >= 4 && kRssT <= 31, "the worker's pick key holds the slot in 5 bits");
 constexpr uint32_t kRssM24 = 0xFFFFFFu;
 struct RsStream {
@@ -2789,7 +2801,14 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // sparse-wave shading threshold divisor (k_path TAIL): 2 -- bench frame,
     // pixel seeding 235.2 -> 231.9 ms at N=1, 1/8 shard unchanged (41.0 ms);
     // sample seeding 220.4 -> 218.2 ms at N=1, 29.4 -> 29.0 ms at 1/8
-    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
+    // (TMPT_PATH_STEPS / TMPT_SHADE_MIN / TMPT_SPARSE: A/B builds, tools/ab_build.sh)
+    constexpr int kPathSL = 16, kPathSteps = TMPT_PATH_STEPS, kShadeMin = TMPT_SHADE_MIN, kSparse = TMPT_SPARSE;
+    // pixel seeding's kernels: 24 rounds between shading checks -- re-swept at
+    // 5 waves per SIMD (whole renders, steps 16 / 24 / 32: 1/8 shard 36.4 /
+    // 35.2 / 36.1 ms, 1/4 63.7 / 63.2 / 65.1, N=1 198.0 / 196.0 / 208.9; the
+    // sample kernels 172.3 / 172.8 / 182.9 keep 16;
+    // profiles/r06_experiments/cadence_5waves*.log)
+    constexpr int kPixSteps = TMPT_PIX_STEPS;
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
     // kernel keeps its register allocation)
@@ -2800,8 +2819,8 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
                                      : k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>)
                               : (soa ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1, true>
                                      : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 1>))
-                     : (count ? k_path<true, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>
-                              : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
+                     : (count ? k_path<true, kBlk, kPathSL, kPixSteps, kShadeMin, 4, kSparse>
+                              : k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 4, kSparse>);
     const PathFn fn_default = fn;
     int prof = 0;
 #ifdef TMPT_DIAG
@@ -2810,9 +2829,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // (more registers: compare its times only among PROF=3 runs)
     if (const char* pe = getenv("TMPT_PROF")) prof = count ? 0 : atoi(pe);
     if (prof && !a.jt)
-        fn = prof >= 3 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 3>
-           : prof == 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 2>
-                       : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 1>;
+        fn = prof >= 3 ? k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 1, kSparse, 3>
+           : prof == 2 ? k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 1, kSparse, 2>
+                       : k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 1, kSparse, 1>;
     if (prof && a.jt)
         fn = prof >= 2 ? k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 2, 0, 1>
                        : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 1, kSparse, 1, 0, 1>;
@@ -2970,16 +2989,16 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     int pair = help && ordered ? (2 * P <= 3 * lanes ? 52 : 56) : 0;
     if (o.pair >= 0) pair = o.pair;
     if (help)
-        fn = waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 1>
-                     : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1>;
+        fn = waves5p ? k_path<false, kBlk, kPathSL5, kPixSteps, kShadeMin, 5, kSparse, 0, 1>
+                     : k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 4, kSparse, 0, 1>;
     else if (waves5p)
-        fn = k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse>;
+        fn = k_path<false, kBlk, kPathSL5, kPixSteps, kShadeMin, 5, kSparse>;
     // pixel seeding with the octree there: the leaves only flag ties (TIES 2)
     if (!a.jt && !count && !prof && s.oct_view && o.tie_rule == 0)
-        fn = help ? (waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 1, 0, false, 2>
-                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>)
-                  : (waves5p ? k_path<false, kBlk, kPathSL5, kPathSteps, kShadeMin, 5, kSparse, 0, 0, 0, false, 2>
-                             : k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>);
+        fn = help ? (waves5p ? k_path<false, kBlk, kPathSL5, kPixSteps, kShadeMin, 5, kSparse, 0, 1, 0, false, 2>
+                             : k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 4, kSparse, 0, 1, 0, false, 2>)
+                  : (waves5p ? k_path<false, kBlk, kPathSL5, kPixSteps, kShadeMin, 5, kSparse, 0, 0, 0, false, 2>
+                             : k_path<false, kBlk, kPathSL, kPixSteps, kShadeMin, 4, kSparse, 0, 0, 0, false, 2>);
     // stack spill areas for either kind of kernel's lanes (4 waves, 16 LDS
     // entries; 5 waves, 12)
     const size_t ovf_words = std::max((size_t)grid4 * (kStackTotal - kPathSL),
