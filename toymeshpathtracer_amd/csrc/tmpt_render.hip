@@ -882,6 +882,12 @@ constexpr int kRssT = TMPT_RSS_T;
 #ifndef TMPT_PIX_STEPS
 #define TMPT_PIX_STEPS 24
 #endif
+#ifndef TMPT_ROW_STEPS
+#define TMPT_ROW_STEPS 16
+#endif
+#ifndef TMPT_ROW_SHADE_MIN
+#define TMPT_ROW_SHADE_MIN 24
+#endif
 #ifndef TMPT_SHADE_MIN
 #define TMPT_SHADE_MIN 16
 #endif
@@ -3277,7 +3283,11 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
 int render_rowstream(Scene& s, const RenderArgs& a, uint32_t* d_out, unsigned long long* d_counters)
 {
     const Options& o = s.opt;
-    constexpr int kPathSL = 16, kPathSteps = 16, kShadeMin = 16, kSparse = 2;
+    // a shading round once 24 lanes wait (16 before round 6): whole row renders,
+    // 16 / 24 / 28 / 32, N=1 1835.9 / 1811.4 / 1811.9 / 1833.8 ms, 1/2 1034.8 /
+    // 1023.5 / 1023.6, 1/8 432.1 / 430.4 / 427.6 / 428.3; 24 or 32 rounds per
+    // check instead of 16: -0.8 / +1.2 % at N=1 (profiles/r06_experiments/row_cadence*.log)
+    constexpr int kPathSL = 16, kPathSteps = TMPT_ROW_STEPS, kShadeMin = TMPT_ROW_SHADE_MIN, kSparse = 2;
     // with the reference's octree answering (tie_rule visit) the leaves only
     // flag a tie and keep the first triangle met (TIES 2): the flagged query's
     // answer comes from the octree either way, so the lowest-index bookkeeping
