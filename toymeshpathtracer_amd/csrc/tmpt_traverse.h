@@ -233,28 +233,7 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
             A = sv.soa.na[k], B = sv.soa.nb[k], L = sv.soa.nd[k];
             const uint2 c2 = sv.soa.nc[k];
             C = make_uint4(c2.x, c2.y, 0u, 0u);
-        }
-#ifdef TMPT_V_FLATNODE  // A/B: one generic (FLAT) load path for LDS top nodes and global nodes
-        else if (TOPC) {
-            const uint4* gp = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
-                                                             ((uint32_t)ts.node << 6));
-            const uint4* lp = (const uint4*)st.top + ((uint32_t)ts.node << 2);  // addrspacecast to generic
-            const uint4* p = (uint32_t)ts.node < st.ntop ? lp : gp;
-            A = p[0], B = p[1], C = p[2];
-            L = reinterpret_cast<const int4*>(p)[3];
-        }
-#endif
-#ifdef TMPT_V_LDSFIRST  // A/B: the LDS branch first in program order
-        else if (TOPC && (uint32_t)ts.node < st.ntop) {
-            const lds_u4* q = st.top + ((uint32_t)ts.node << 2);
-            const u32x4 a4 = q[0], b4 = q[1], c4 = q[2], l4 = q[3];
-            A = make_uint4(a4.x, a4.y, a4.z, a4.w);
-            B = make_uint4(b4.x, b4.y, b4.z, b4.w);
-            C = make_uint4(c4.x, c4.y, c4.z, c4.w);
-            L = make_int4((int)l4.x, (int)l4.y, (int)l4.z, (int)l4.w);
-        }
-#endif
-        else if (!TOPC || (uint32_t)ts.node >= st.ntop) {
+        } else if (!TOPC || (uint32_t)ts.node >= st.ntop) {
             const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sv.nodes4) +
                                                             ((uint32_t)ts.node << 6));
             A = p[0], B = p[1], C = p[2];
@@ -424,9 +403,6 @@ __device__ __forceinline__ bool trav_step4q2_mixed(const SceneView& sv, const Tr
     }
     if (ts.sp == 0) return true;
     ts.node = st.pop(ts.sp);
-#ifdef TMPT_V_POPWAIT  // A/B: the popped value is waited for inside the pop path, not at the join
-    asm volatile("" : "+v"(ts.node));
-#endif
     return false;
 }
 
