@@ -2812,8 +2812,9 @@ int render_persistent(Scene& s, const RenderArgs& a, uint32_t* d_out, bool count
     // pixel seeding's kernels: 24 rounds between shading checks -- re-swept at
     // 5 waves per SIMD (whole renders, steps 16 / 24 / 32: 1/8 shard 36.4 /
     // 35.2 / 36.1 ms, 1/4 63.7 / 63.2 / 65.1, N=1 198.0 / 196.0 / 208.9; the
-    // sample kernels 172.3 / 172.8 / 182.9 keep 16;
-    // profiles/r06_experiments/cadence_5waves*.log)
+    // sample kernels 172.3 / 172.8 / 182.9 keep 16; 20 and 28 both lose to 24,
+    // +1.4 % at 1/8; profiles/r06_experiments/cadence_5waves*.log,
+    // cadence_pixel_20_24_28.log)
     constexpr int kPixSteps = TMPT_PIX_STEPS;
     using PathFn = decltype(&k_path<false, kBlk, kPathSL, kPathSteps, kShadeMin, 4, kSparse>);
     // pixel seeding, and sample seeding (its own instantiation: the pixel-mode
